@@ -1,0 +1,199 @@
+"""Throughput bench of the region-proposal + RoI hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
+
+One "step" = one pass of the hot path over one batch of synthetic VOC-shaped
+input already resident in HBM (BASELINE.json configs[1] = cfg2: 8 images of
+600x1000, stride-16 38x63x9 anchors, 6000->300 NMS@0.7, RoIPool 7x7x256):
+
+    propose (decode+clamp+filter+top-k+NMS+post, anchors generated in-kernel)
+    -> RoI transform (nets/heads.py:42-47) -> RoIPool forward
+
+For N>1 (torch.distributed.run, one process per GPU) every rank runs its own
+batch of 8 images (weak scaling, images seeded by global index) and the
+padded detections are all-gathered over RCCL at the end of each step -- the
+only collective on this path.
+
+Prints ONE JSON line (rank 0) with the metric of BASELINE.json plus
+"roofline" (RoIPool forward, achieved algorithmic HBM GB/s from HIP events
+vs the 8 TB/s peak) and "cpu_baseline" (the oracle CPU path on this host).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="bounded CPU-baseline sample (rank 0, N=1 only); 0 disables")
+    return ap.parse_args()
+
+
+def setup_dist(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def make_inputs(cfg, batch, first_image, device):
+    from replication_faster_rcnn_amd import synth
+    c = synth.CONFIGS[cfg]
+    K = 3 * len(c["scales"])
+    A = c["feat_h"] * c["feat_w"] * K
+    imgs = range(first_image, first_image + batch)
+    sc = torch.from_numpy(np.stack([synth.rpn_scores(A, 0, i) for i in imgs])).to(device)
+    de = torch.from_numpy(np.stack([synth.rpn_deltas(A, 0, i) for i in imgs])).to(device)
+    x = torch.from_numpy(np.stack([synth.features(c["C"], c["feat_h"], c["feat_w"], 0, i)
+                                   for i in imgs])).to(device)
+    return c, sc, de, x
+
+
+def cpu_baseline(cfg, seconds):
+    """Oracle CPU path (numpy restatement + single-threaded C nms/roi_pool,
+    the reference's own per-image loop nets/rpn.py:131) on a bounded sample."""
+    from oracle import ref_numpy as orc
+    from replication_faster_rcnn_amd import synth
+    c = synth.CONFIGS[cfg]
+    base = orc.generate_anchor_base(anchor_scales=c["scales"])
+    done, t0, i = 0, time.perf_counter(), 0
+    warm = True
+    while True:
+        anchors = orc.generate_anchors(base, 16, c["feat_w"], c["feat_h"])
+        A = len(anchors)
+        sc, de = synth.rpn_scores(A, 0, i), synth.rpn_deltas(A, 0, i)
+        x = synth.features(c["C"], c["feat_h"], c["feat_w"], 0, i)[None]
+        if warm:
+            t0 = time.perf_counter()
+        ts = time.perf_counter()
+        rois, _ = orc.propose_one(anchors, sc, de, c["img_w"], c["img_h"], c["pre_nms"], c["post_nms"])
+        boxes = orc.roi_transform(rois, np.zeros(len(rois), np.float32), c["img_h"], c["img_w"],
+                                  c["feat_h"], c["feat_w"])
+        orc.roi_pool_forward(x, boxes, 7, 1.0)
+        te = time.perf_counter()
+        if warm:
+            warm = False
+            t0 = te
+            continue
+        done += 1
+        i += 1
+        if te - t0 >= seconds:
+            break
+    el = time.perf_counter() - t0
+    return {"value": done / el, "unit": "images/sec", "cores": 1, "kind": "port",
+            "sample": f"{done} {cfg}-shaped images, one at a time (oracle: numpy + 1-thread C "
+                      f"nms/roi_pool), after 1 warm-up image; {el:.1f} s on {os.cpu_count()}-cpu host"}
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args.gpus)
+    dev = torch.device("cuda", local)
+    from replication_faster_rcnn_amd import anchors as A, ops
+    c, sc, de, x = make_inputs(args.config, c_batch(args.config), rank * c_batch(args.config), dev)
+    N = sc.size(0)
+    base = A.generate_anchor_base_device(anchor_scales=c["scales"])
+    post = c["post_nms"]
+    inds = torch.arange(N, device=dev, dtype=torch.float32).repeat_interleave(post)
+    if world > 1:
+        g_rois = torch.empty((world * N, post, 4), device=dev)
+        g_idx = torch.empty((world * N, post), dtype=torch.int32, device=dev)
+        g_cnt = torch.empty((world * N,), dtype=torch.int32, device=dev)
+    ev = []
+
+    def step(timed):
+        rois, idx, cnt = ops.propose(sc, de, img_w=c["img_w"], img_h=c["img_h"],
+                                     pre_nms=c["pre_nms"], post_nms=post, anchor_base=base,
+                                     feat_h=c["feat_h"], feat_w=c["feat_w"])
+        boxes = ops.roi_transform(rois.view(-1, 4), inds, c["img_h"], c["img_w"], c["feat_h"],
+                                  c["feat_w"])
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        pooled, am = ops._roi_pool_fwd(x, boxes, 7, 7, 1.0)
+        if timed:
+            e1.record()
+            ev.append((e0, e1))
+        if world > 1:
+            dist.all_gather_into_tensor(g_rois, rois)
+            dist.all_gather_into_tensor(g_idx, idx)
+            dist.all_gather_into_tensor(g_cnt, cnt)
+        return cnt
+
+    for _ in range(args.warmup):
+        cnt = step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        cnt = step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    roi_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    R = int(cnt.sum().item())
+    C, H, W = x.shape[1:]
+    alg_bytes = N * C * H * W * 4 + R * 20 + 2 * R * C * 49 * 4
+    achieved = alg_bytes / (roi_ms * 1e-3) / 1e9
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "roi_pool_fwd_traffic.json")
+    if os.path.exists(tpath):
+        traffic = json.load(open(tpath)).get(args.config, {}).get("hbm_bytes_per_launch")
+    images = world * N * args.steps
+    rec = {
+        "metric": "images/sec through RPN proposal+NMS+RoIPool; RoIPool HBM GB/s vs peak",
+        "value": images / el, "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+        "config": {"workload": f"{args.config}: {N} VOC-shape images/GPU 600x1000, 38x63x9 anchors, "
+                               f"{c['pre_nms']}->{post} NMS@0.7, RoIPool 7x7x{C}",
+                   "global_batch": world * N, "parallelism": f"dp{world} (per-image sharding)"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "roi_pool_fwd_kernel", "kernel_us": roi_ms * 1e3,
+                     "alg_bytes_per_launch": alg_bytes},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        rec["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
+        rec["cpu_baseline"]["gpu_over_cpu"] = rec["value"] / rec["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def c_batch(cfg):
+    from replication_faster_rcnn_amd import synth
+    return synth.CONFIGS[cfg]["batch"]
+
+
+if __name__ == "__main__":
+    main()

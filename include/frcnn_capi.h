@@ -1,0 +1,125 @@
+/*
+ * frcnn_capi.h -- C-ABI of the MI355X-native region-proposal + RoI hot path.
+ *
+ * This is the drop-in boundary.  Every entry point:
+ *   - is extern "C", takes plain pointers / sizes, no torch types;
+ *   - takes caller-owned DEVICE buffers (unless a parameter says "host");
+ *   - is stream-ordered and asynchronous on `stream` (a hipStream_t, passed
+ *     as void*; NULL = the default stream), never synchronises, never
+ *     allocates (workspace comes from the caller, sized by the matching
+ *     *_workspace_size() query), so a sequence of calls can be captured in a
+ *     hipGraph;
+ *   - returns 0 on success or a negative FRCNN_E* code, never throws across
+ *     the ABI; frcnn_last_error() returns a message for the calling thread.
+ *
+ * Each function cites the reference interface it replaces (file:line in
+ * juniorliu95/replication_faster_rcnn, or the torchvision op the reference
+ * calls at that line).  Numerics: see DESIGN.md "Parity contract".
+ */
+#ifndef FRCNN_CAPI_H_
+#define FRCNN_CAPI_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FRCNN_OK 0
+#define FRCNN_EINVAL (-1)     /* bad shape / argument */
+#define FRCNN_EHIP (-2)       /* HIP runtime error (launch failure) */
+#define FRCNN_EWORKSPACE (-3) /* workspace too small */
+
+const char* frcnn_version(void);
+const char* frcnn_last_error(void);
+
+/* ---------------------------------------------------------------- anchors */
+
+/* utils/anchors.py:5 generate_anchor_base(base_size, ratios, anchor_scales).
+ * ratios / scales are HOST arrays (n_ratios*n_scales <= 64).  out_base: device
+ * fp32 [n_ratios*n_scales, 4], row r*n_scales+s. */
+int frcnn_anchor_base(const double* ratios, int n_ratios, const double* scales, int n_scales,
+                      double base_size, float* out_base, void* stream);
+
+/* utils/anchors.py:33 generate_anchors(anchor_base, feat_stride, width, height).
+ * anchor_base fp32 [K,4]; out fp32 [height*width*K, 4]. */
+int frcnn_generate_anchors(const float* anchor_base, int K, int feat_stride, int width,
+                           int height, float* out, void* stream);
+
+/* utils/utils.py:47 reg2bbox(anchors, reg): fp32 [n,4] x [n,4] -> [n,4]. */
+int frcnn_reg2bbox(const float* anchors, const float* reg, int64_t n, float* out, void* stream);
+
+/* ------------------------------------------------------------- proposals */
+
+/* Parameters of the batched proposal layer (nets/rpn.py:22-45 kwargs). */
+typedef struct frcnn_propose_params {
+    int N;            /* images in the batch */
+    int A;            /* anchors per image */
+    int K;            /* anchors per location (used when anchors == NULL) */
+    int feat_h;       /* feature map height   (used when anchors == NULL) */
+    int feat_w;       /* feature map width    (used when anchors == NULL) */
+    int feat_stride;  /* 16                   (used when anchors == NULL) */
+    float img_h;      /* clamp bound of box columns 0,2 (nets/rpn.py:62) */
+    float img_w;      /* clamp bound of box columns 1,3 (nets/rpn.py:63) */
+    float min_size;   /* nets/rpn.py:27,65 */
+    int pre_nms;      /* nets/rpn.py:39-43 */
+    int post_nms;     /* nets/rpn.py:40-43 */
+    double iou_threshold; /* nets/rpn.py:44 */
+} frcnn_propose_params;
+
+size_t frcnn_propose_workspace_size(const frcnn_propose_params* p);
+
+/* nets/rpn.py:47-79 region_proposal.__call__, batched over N images
+ * (replaces the per-image loop nets/rpn.py:131-136).
+ *   scores  fp32 [N, A]     fg softmax (nets/rpn.py:119)
+ *   deltas  fp32 [N, A, 4]  RPN reg    (nets/rpn.py:124)
+ *   anchors fp32 [A, 4] or NULL; if NULL, anchors are generated in-kernel from
+ *           anchor_base fp32 [K,4] on the feat_h x feat_w grid (A = feat_h*feat_w*K)
+ * Outputs (padded to post_nms):
+ *   out_rois  fp32 [N, post_nms, 4]   rows >= out_count[n] are zero
+ *   out_idx   int32 [N, post_nms]     anchor index of each roi, -1 padding
+ *   out_count int32 [N]               min(post_nms, #kept by NMS) */
+int frcnn_propose(const frcnn_propose_params* p, const float* scores, const float* deltas,
+                  const float* anchors, const float* anchor_base, float* out_rois,
+                  int32_t* out_idx, int32_t* out_count, void* workspace, size_t ws_bytes,
+                  void* stream);
+
+/* torchvision.ops.nms(boxes, scores, iou_threshold) as called at nets/rpn.py:75.
+ *   boxes fp32 [n,4] (x1,y1,x2,y2), scores fp32 [n]
+ *   keep int64 [n]: kept indices in descending-score order; *count (device
+ *   int32) = number kept. */
+size_t frcnn_nms_workspace_size(int64_t n);
+int frcnn_nms(const float* boxes, const float* scores, int64_t n, double iou_threshold,
+              int64_t* keep, int32_t* count, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------- RoIPool */
+
+/* nets/heads.py:42-47: image-space rois fp32 [R,4] + roi_inds fp32 [R] ->
+ * boxes fp32 [R,5] = [idx, r0/img_h*feat_h, r1/img_w*feat_w, r2/img_h*feat_h,
+ * r3/img_w*feat_w]. */
+int frcnn_roi_transform(const float* rois, const float* roi_inds, int64_t R, float img_h,
+                        float img_w, int feat_h, int feat_w, float* boxes, void* stream);
+
+/* torchvision.ops.roi_pool forward (nets/heads.py:48):
+ *   x fp32 [N,C,H,W], rois fp32 [R,5] -> out fp32 [R,C,PH,PW],
+ *   argmax int32 [R,C,PH,PW] (h*W+w within the plane, -1 for empty bins).
+ * RoIs whose batch index is outside [0,N) produce 0 / -1. */
+int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
+                       int PH, int PW, float spatial_scale, float* out, int32_t* argmax,
+                       void* stream);
+
+/* torchvision _roi_pool_backward (autograd of nets/heads.py:48, reached from
+ * train.py:126):  grad_in fp32 [N,C,H,W] = 0, then for n, c, ph, pw in order
+ * grad_in[b(n), c, argmax] += grad[n, c, ph, pw].  Deterministic, atomic-free,
+ * same summation order as the CPU kernel. */
+size_t frcnn_roi_pool_bwd_workspace_size(int64_t R, int N, int PH, int PW);
+int frcnn_roi_pool_bwd(const float* grad, const float* rois, const int32_t* argmax, int64_t R,
+                       int N, int C, int H, int W, int PH, int PW, float spatial_scale,
+                       float* grad_in, void* workspace, size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FRCNN_CAPI_H_ */

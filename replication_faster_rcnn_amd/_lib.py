@@ -1,0 +1,102 @@
+"""ctypes binding of the C-ABI library ``libfrcnn_mi355x.so`` (include/frcnn_capi.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (or ``make -C
+replication_faster_rcnn_amd/csrc``).  There is no CPU fallback: if the
+library is missing or no GPU is visible, every op raises.
+
+torch is imported before the library is loaded so that the library's
+``libamdhip64.so.7`` dependency resolves to the HIP runtime torch already
+loaded (same soname): one runtime, one device-pointer space, torch streams
+usable directly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfrcnn_mi355x.so")
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int
+I64 = ctypes.c_int64
+F32 = ctypes.c_float
+F64 = ctypes.c_double
+SZ = ctypes.c_size_t
+
+
+class ProposeParams(ctypes.Structure):
+    """frcnn_propose_params (include/frcnn_capi.h)."""
+
+    _fields_ = [("N", I32), ("A", I32), ("K", I32), ("feat_h", I32), ("feat_w", I32),
+                ("feat_stride", I32), ("img_h", F32), ("img_w", F32), ("min_size", F32),
+                ("pre_nms", I32), ("post_nms", I32), ("iou_threshold", F64)]
+
+
+# name -> (restype, argtypes); must match include/frcnn_capi.h exactly
+SIGNATURES = {
+    "frcnn_version": (ctypes.c_char_p, []),
+    "frcnn_last_error": (ctypes.c_char_p, []),
+    "frcnn_anchor_base": (I32, [P, I32, P, I32, F64, P, P]),
+    "frcnn_generate_anchors": (I32, [P, I32, I32, I32, I32, P, P]),
+    "frcnn_reg2bbox": (I32, [P, P, I64, P, P]),
+    "frcnn_propose_workspace_size": (SZ, [ctypes.POINTER(ProposeParams)]),
+    "frcnn_propose": (I32, [ctypes.POINTER(ProposeParams), P, P, P, P, P, P, P, P, SZ, P]),
+    "frcnn_nms_workspace_size": (SZ, [I64]),
+    "frcnn_nms": (I32, [P, P, I64, F64, P, P, P, SZ, P]),
+    "frcnn_roi_transform": (I32, [P, P, I64, F32, F32, I32, I32, P, P]),
+    "frcnn_roi_pool_fwd": (I32, [P, P, I64, I32, I32, I32, I32, I32, I32, F32, P, P, P]),
+    "frcnn_roi_pool_bwd_workspace_size": (SZ, [I64, I32, I32, I32]),
+    "frcnn_roi_pool_bwd": (I32, [P, P, P, I64, I32, I32, I32, I32, I32, I32, F32, P, P, SZ, P]),
+}
+
+_lib = None
+
+
+class FrcnnError(RuntimeError):
+    pass
+
+
+def load(require_gpu: bool = True):
+    """Load the library (raises FrcnnError if it was not built).  With
+    ``require_gpu`` also insist that a HIP device is visible."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FrcnnError(f"HIP library not built: {LIB_PATH} missing "
+                             "(run __graft_entry__.build() or make -C replication_faster_rcnn_amd/csrc)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    if require_gpu and not torch.cuda.is_available():
+        raise FrcnnError("replication_faster_rcnn_amd needs an MI355X (no HIP device visible); "
+                         "there is no CPU fallback")
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = _lib.frcnn_last_error().decode()
+        raise FrcnnError(f"{what} failed (rc={rc}): {msg}")
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def device():
+    """The device the HIP path runs on (current CUDA/HIP device)."""
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def workspace(nbytes: int, dev) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)

@@ -1,0 +1,521 @@
+// Proposal layer (nets/rpn.py:47-79) and torchvision-style NMS on gfx950.
+//
+// Pipeline, one launch each, batched over images (blockIdx.y / blockIdx.x = image):
+//   1. decode_filter  : anchors (generated in-register) + deltas -> decoded,
+//                       clamped boxes; min-size mask; 64-bit sort key
+//                       (desc score : anchor index) -- nets/rpn.py:58-68
+//   2. select         : wave64-ballot radix select of the pre_nms-th key, one
+//                       1024-thread workgroup per image -- nets/rpn.py:71-72
+//   3. compact        : keys <= threshold appended to a per-image list
+//   4. rank           : rank = #smaller keys (keys are unique), scatter boxes
+//                       into score order -- nets/rpn.py:71-74
+//   5. nms_mask       : 64x64 IoU tiles of the upper triangle -> bitmask,
+//                       stored column-block-major maskT[cb][i]
+//   6. nms_sweep      : greedy resolution per image, one workgroup; a wave
+//                       resolves each 64-box block serially in SGPRs; stops
+//                       as soon as post_nms boxes are kept -- nets/rpn.py:75-77
+// Ties in score are ordered by ascending anchor index (documented deviation:
+// the reference's CPU argsort is unstable under ties).
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+
+#include "common.h"
+
+namespace frcnn {
+
+// Exact form of torchvision's `(double)(inter / union) > iou_threshold`.
+struct NmsThr {
+    double thr;    // the raw threshold
+    double mid;    // midpoint below the smallest float T with (double)T > thr
+    int tie_incl;  // a quotient equal to `mid` rounds up to T
+    int never;     // thr is NaN: nothing is ever suppressed
+};
+
+static NmsThr make_thr(double thr) {
+    NmsThr t{};
+    t.thr = thr;
+    if (std::isnan(thr)) {
+        t.never = 1;
+        return t;
+    }
+    float f = static_cast<float>(thr);
+    if (!(static_cast<double>(f) > thr)) f = std::nextafter(f, INFINITY);
+    if (std::isinf(f) && f > 0) {
+        t.mid = std::ldexp(1.0, 128) - std::ldexp(1.0, 103);  // overflow boundary, ties to inf
+        t.tie_incl = 1;
+        return t;
+    }
+    float pred = std::nextafter(f, -INFINITY);
+    t.mid = (static_cast<double>(pred) + static_cast<double>(f)) * 0.5;
+    uint32_t bits;
+    std::memcpy(&bits, &f, 4);
+    t.tie_incl = (bits & 1u) == 0;
+    return t;
+}
+
+// IoU(a, b) > thr with torchvision's fp32 op order.
+// Fast path: RN(inter/uni) > thr  <=>  inter >= mid*uni  (exact in fp64, since
+// mid has <= 25 and uni 24 significant bits), valid for finite uni > 0.
+__device__ __forceinline__ bool iou_over(float4 a, float aarea, float4 b, float barea,
+                                         const NmsThr& t) {
+    float xx1 = a.x < b.x ? b.x : a.x;
+    float yy1 = a.y < b.y ? b.y : a.y;
+    float xx2 = b.z < a.z ? b.z : a.z;
+    float yy2 = b.w < a.w ? b.w : a.w;
+    float w = xx2 - xx1;
+    float h = yy2 - yy1;
+    w = 0.0f < w ? w : 0.0f;
+    h = 0.0f < h ? h : 0.0f;
+    float inter = w * h;
+    float uni = aarea + barea;
+    uni = uni - inter;
+    if (uni > 0.0f && uni <= FLT_MAX && inter <= FLT_MAX) {
+        double lhs = static_cast<double>(inter);
+        double rhs = t.mid * static_cast<double>(uni);
+        return lhs > rhs || (t.tie_incl && lhs == rhs);
+    }
+    float ovr = inter / uni;
+    return static_cast<double>(ovr) > t.thr;
+}
+
+__device__ __forceinline__ float box_area(float4 b) {
+    float dx = b.z - b.x;
+    float dy = b.w - b.y;
+    return dx * dy;
+}
+
+constexpr uint64_t kInvalidKey = ~0ull;
+
+// ---------------------------------------------------------------- 1. decode
+__global__ __launch_bounds__(256) void decode_filter_kernel(
+    const float* __restrict__ scores, const float4* __restrict__ deltas,
+    const float4* __restrict__ anchors, const float4* __restrict__ base, int A, int K, int W,
+    int stride, float img_h, float img_w, float min_size, float4* __restrict__ boxes,
+    uint64_t* __restrict__ keys) {
+    int a = blockIdx.x * 256 + threadIdx.x;
+    if (a >= A) return;
+    size_t o = static_cast<size_t>(blockIdx.y) * A + a;
+    float4 an;
+    if (anchors) {
+        an = anchors[a];
+    } else {  // utils/anchors.py:46-59 in-register
+        int k = a % K;
+        int cell = a / K;
+        float sx = static_cast<float>(stride * (cell % W));
+        float sy = static_cast<float>(stride * (cell / W));
+        float4 bb = base[k];
+        an = make_float4(bb.x + sx, bb.y + sy, bb.z + sx, bb.w + sy);
+    }
+    float4 b = decode_box(an, deltas[o]);
+    b.x = clamp_nan(b.x, 0.0f, img_h);
+    b.z = clamp_nan(b.z, 0.0f, img_h);
+    b.y = clamp_nan(b.y, 0.0f, img_w);
+    b.w = clamp_nan(b.w, 0.0f, img_w);
+    bool ok = (b.z - b.x >= min_size) && (b.w - b.y >= min_size);
+    boxes[o] = b;
+    keys[o] = ok ? (static_cast<uint64_t>(desc_score_key(scores[o])) << 32) | static_cast<uint32_t>(a)
+                 : kInvalidKey;
+}
+
+// keys for the plain nms op: every box valid, index order breaks ties.
+__global__ __launch_bounds__(256) void nms_keys_kernel(const float* __restrict__ scores, int n,
+                                                       uint64_t* __restrict__ keys) {
+    int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = (static_cast<uint64_t>(desc_score_key(scores[i])) << 32) | static_cast<uint32_t>(i);
+}
+
+// ---------------------------------------------------------------- 2. select
+// One 1024-thread workgroup per image.  Finds T = the K-th smallest valid key
+// (K = min(#valid, pre)), MSB-first over 8-bit digits; per-digit histograms
+// are built with one LDS atomic per (wave, distinct digit) via ballots.
+__global__ __launch_bounds__(1024) void select_kernel(const uint64_t* __restrict__ keys_all, int A,
+                                                      int pre, uint64_t* __restrict__ sel_T,
+                                                      int* __restrict__ sel_P,
+                                                      unsigned* __restrict__ list_cnt) {
+    const int n = blockIdx.x;
+    const uint64_t* keys = keys_all + static_cast<size_t>(n) * A;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    __shared__ unsigned hist[256];
+    __shared__ unsigned s_part[16];
+    __shared__ unsigned s_digit, s_before, s_bucket;
+
+    unsigned c = 0;
+    for (int i = tid; i < A; i += 1024) c += keys[i] != kInvalidKey;
+    c = wave_sum_u32(c);
+    if (lane == 0) s_part[wid] = c;
+    __syncthreads();
+    unsigned M = 0;
+    for (int w = 0; w < 16; ++w) M += s_part[w];
+    const unsigned Kc = M < static_cast<unsigned>(pre) ? M : static_cast<unsigned>(pre);
+    if (tid == 0) {
+        list_cnt[n] = 0;
+        sel_P[n] = static_cast<int>(Kc);
+    }
+    if (Kc == M) {  // everything valid is selected
+        if (tid == 0) sel_T[n] = kInvalidKey - 1;
+        return;
+    }
+    uint64_t prefix = 0;
+    unsigned need = Kc;
+    uint64_t T = 0;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+        if (tid < 256) hist[tid] = 0;
+        __syncthreads();
+        const uint64_t himask = shift == 56 ? 0ull : (~0ull << (shift + 8));
+        for (int i0 = 0; i0 < A; i0 += 1024) {
+            int i = i0 + tid;
+            uint64_t k = i < A ? keys[i] : kInvalidKey;
+            bool m = k != kInvalidKey && (k & himask) == prefix;
+            unsigned d = static_cast<unsigned>(k >> shift) & 255u;
+            uint64_t act = __ballot(m);
+            while (act) {
+                int leader = __ffsll(static_cast<unsigned long long>(act)) - 1;
+                unsigned dl = __builtin_amdgcn_readlane(d, leader);
+                uint64_t same = __ballot(m && d == dl);
+                if (lane == leader) atomicAdd(&hist[dl], static_cast<unsigned>(__popcll(same)));
+                act &= ~same;
+            }
+        }
+        __syncthreads();
+        if (wid == 0) {
+            unsigned h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2],
+                     h3 = hist[4 * lane + 3];
+            unsigned tot = h0 + h1 + h2 + h3;
+            unsigned incl = tot;  // inclusive wave scan
+            for (int o = 1; o < 64; o <<= 1) {
+                unsigned v = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += v;
+            }
+            unsigned before = incl - tot;
+            unsigned hv[4] = {h0, h1, h2, h3};
+            for (int q = 0; q < 4; ++q) {
+                if (before < need && before + hv[q] >= need) {
+                    s_digit = 4 * lane + q;
+                    s_before = before;
+                    s_bucket = hv[q];
+                }
+                before += hv[q];
+            }
+        }
+        __syncthreads();
+        unsigned d = s_digit;
+        need -= s_before;
+        prefix |= static_cast<uint64_t>(d) << shift;
+        if (s_bucket == need) {  // the whole bucket is taken
+            T = prefix | ((1ull << shift) - 1ull);
+            break;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) sel_T[n] = T;
+}
+
+// --------------------------------------------------------------- 3. compact
+__global__ __launch_bounds__(256) void compact_kernel(const uint64_t* __restrict__ keys_all, int A,
+                                                      int pre, const uint64_t* __restrict__ sel_T,
+                                                      unsigned* __restrict__ list_cnt,
+                                                      uint64_t* __restrict__ list_keys) {
+    const int n = blockIdx.y;
+    const int a = blockIdx.x * 256 + threadIdx.x;
+    const uint64_t T = sel_T[n];
+    uint64_t k = a < A ? keys_all[static_cast<size_t>(n) * A + a] : kInvalidKey;
+    bool m = k != kInvalidKey && k <= T;
+    uint64_t act = __ballot(m);
+    if (!act) return;
+    int leader = __ffsll(static_cast<unsigned long long>(act)) - 1;
+    unsigned base = 0;
+    if (lane_id() == leader) base = atomicAdd(&list_cnt[n], static_cast<unsigned>(__popcll(act)));
+    base = __shfl(base, leader, 64);
+    if (m) list_keys[static_cast<size_t>(n) * pre + base + __popcll(act & lanemask_lt())] = k;
+}
+
+// ------------------------------------------------------------------ 4. rank
+// 64 candidates per workgroup, the 4 waves split the comparison range.
+__global__ __launch_bounds__(256) void rank_kernel(const uint64_t* __restrict__ list_keys, int pre,
+                                                   const int* __restrict__ sel_P,
+                                                   const float4* __restrict__ box_src, int A,
+                                                   float4* __restrict__ sbox,
+                                                   int32_t* __restrict__ sidx) {
+    const int n = blockIdx.y;
+    const int P = sel_P[n];
+    const int i0 = blockIdx.x * 64;
+    if (i0 >= P) return;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t* lk = list_keys + static_cast<size_t>(n) * pre;
+    __shared__ uint64_t tile[1024];
+    __shared__ unsigned part[4][64];
+    const int i = i0 + lane;
+    const uint64_t ki = i < P ? lk[i] : kInvalidKey;
+    unsigned cnt = 0;
+    for (int t0 = 0; t0 < P; t0 += 1024) {
+        for (int q = tid; q < 1024; q += 256) tile[q] = (t0 + q < P) ? lk[t0 + q] : kInvalidKey;
+        __syncthreads();
+        const uint64_t* tw = tile + wid * 256;
+#pragma unroll 8
+        for (int j = 0; j < 256; ++j) cnt += tw[j] < ki;
+        __syncthreads();
+    }
+    part[wid][lane] = cnt;
+    __syncthreads();
+    if (wid == 0 && i < P) {
+        unsigned r = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
+        uint32_t a = static_cast<uint32_t>(ki);
+        sidx[static_cast<size_t>(n) * pre + r] = static_cast<int32_t>(a);
+        sbox[static_cast<size_t>(n) * pre + r] = box_src[static_cast<size_t>(n) * A + a];
+    }
+}
+
+// -------------------------------------------------------------- 5. nms mask
+// Upper-triangle tile t -> (row block rb, col block cb >= rb).
+__device__ __forceinline__ void tri_tile(int t, int nb, int& rb, int& cb) {
+    int total = nb * (nb + 1) / 2;
+    int tr = total - 1 - t;  // reversed: row lengths 1, 2, 3, ...
+    int r = static_cast<int>((sqrt(8.0 * tr + 1.0) - 1.0) * 0.5);
+    while ((r + 1) * (r + 2) / 2 <= tr) ++r;
+    while (r * (r + 1) / 2 > tr) --r;
+    int off = tr - r * (r + 1) / 2;
+    rb = nb - 1 - r;
+    cb = nb - 1 - off;
+}
+
+__global__ __launch_bounds__(64) void nms_mask_kernel(const float4* __restrict__ sbox_all, int pre,
+                                                      int Wc, const int* __restrict__ sel_P,
+                                                      NmsThr thr, uint64_t* __restrict__ maskT) {
+    const int n = blockIdx.y;
+    const int P = sel_P[n];
+    const int nbP = (P + 63) / 64;
+    int rb, cb;
+    tri_tile(blockIdx.x, Wc, rb, cb);
+    if (rb >= nbP || cb >= nbP) return;
+    const float4* sbox = sbox_all + static_cast<size_t>(n) * pre;
+    const int lane = threadIdx.x;
+    __shared__ float4 cbox[64];
+    __shared__ float carea[64];
+    const int j = cb * 64 + lane;
+    if (j < P) {
+        float4 b = sbox[j];
+        cbox[lane] = b;
+        carea[lane] = box_area(b);
+    }
+    __syncthreads();
+    const int i = rb * 64 + lane;
+    if (i >= P) return;
+    uint64_t bits = 0;
+    if (!thr.never) {
+        float4 bi = sbox[i];
+        float ai = box_area(bi);
+        int jend = P - cb * 64;
+        jend = jend < 64 ? jend : 64;
+        int jstart = rb == cb ? lane + 1 : 0;
+        for (int jj = jstart; jj < jend; ++jj)
+            if (iou_over(bi, ai, cbox[jj], carea[jj], thr)) bits |= 1ull << jj;
+    }
+    maskT[(static_cast<size_t>(n) * Wc + cb) * pre + i] = bits;
+}
+
+// ------------------------------------------------------------- 6. nms sweep
+// OUT_MODE 0: propose outputs (boxes + int32 anchor index, zero padding);
+// OUT_MODE 1: nms op output (int64 index into the original box array).
+template <int OUT_MODE>
+__global__ __launch_bounds__(256) void nms_sweep_kernel(
+    const uint64_t* __restrict__ maskT_all, const float4* __restrict__ sbox_all,
+    const int32_t* __restrict__ sidx_all, int pre, int Wc, const int* __restrict__ sel_P,
+    int post, float4* __restrict__ out_rois, int32_t* __restrict__ out_idx,
+    int64_t* __restrict__ out_keep, int32_t* __restrict__ out_count) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t kept_bits[];  // [Wc]
+    __shared__ uint64_t red[4];
+    __shared__ int s_count;
+    const int n = blockIdx.x;
+    const int P = sel_P[n];
+    const int nb = (P + 63) / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t* maskT = maskT_all + static_cast<size_t>(n) * Wc * pre;
+    const float4* sbox = sbox_all + static_cast<size_t>(n) * pre;
+    const int32_t* sidx = sidx_all + static_cast<size_t>(n) * pre;
+    if (tid == 0) s_count = 0;
+    __syncthreads();
+    int count = 0;
+    for (int b = 0; b < nb && count < post; ++b) {
+        const uint64_t* col = maskT + static_cast<size_t>(b) * pre;
+        uint64_t acc = 0;
+        for (int i = tid; i < 64 * b; i += 256)
+            if ((kept_bits[i >> 6] >> (i & 63)) & 1ull) acc |= col[i];
+        acc = wave_or_u64(acc);
+        if (lane == 0) red[wid] = acc;
+        __syncthreads();
+        if (wid == 0) {
+            uint64_t removed = red[0] | red[1] | red[2] | red[3];
+            int rows = P - 64 * b;
+            if (rows < 64) removed |= ~0ull << rows;
+            uint64_t diag = lane < rows ? col[64 * b + lane] : 0ull;
+            uint64_t avail = ~removed;
+            uint64_t kept = 0;
+            int cnt = count;
+            while (avail && cnt < post) {
+                int l = __builtin_amdgcn_readfirstlane(__ffsll(static_cast<unsigned long long>(avail)) - 1);
+                kept |= 1ull << l;
+                ++cnt;
+                avail &= ~(readlane_u64(diag, l) | (1ull << l));
+            }
+            if (lane == 0) kept_bits[b] = kept;
+            if ((kept >> lane) & 1ull) {
+                int slot = count + __popcll(kept & lanemask_lt());
+                int r = 64 * b + lane;
+                if (OUT_MODE == 0) {
+                    out_rois[static_cast<size_t>(n) * post + slot] = sbox[r];
+                    out_idx[static_cast<size_t>(n) * post + slot] = sidx[r];
+                } else {
+                    out_keep[slot] = sidx[r];
+                }
+            }
+            if (lane == 0) s_count = cnt;
+        }
+        __syncthreads();
+        count = s_count;
+    }
+    if (OUT_MODE == 0) {
+        for (int s = count + tid; s < post; s += 256) {
+            out_rois[static_cast<size_t>(n) * post + s] = make_float4(0.f, 0.f, 0.f, 0.f);
+            out_idx[static_cast<size_t>(n) * post + s] = -1;
+        }
+    }
+    if (tid == 0) out_count[n] = count;
+}
+
+// ------------------------------------------------------------ workspace map
+struct ProposeWs {
+    uint64_t* keys;
+    float4* boxes;
+    uint64_t* sel_T;
+    int* sel_P;
+    unsigned* list_cnt;
+    uint64_t* list_keys;
+    float4* sbox;
+    int32_t* sidx;
+    uint64_t* maskT;
+    size_t bytes;
+};
+
+static ProposeWs carve(void* ws, int N, int A, int pre, bool need_boxes) {
+    Carver c(ws);
+    ProposeWs w{};
+    const int Wc = (pre + 63) / 64;
+    w.keys = c.take<uint64_t>(static_cast<size_t>(N) * A);
+    w.boxes = need_boxes ? c.take<float4>(static_cast<size_t>(N) * A) : nullptr;
+    w.sel_T = c.take<uint64_t>(N);
+    w.sel_P = c.take<int>(N);
+    w.list_cnt = c.take<unsigned>(N);
+    w.list_keys = c.take<uint64_t>(static_cast<size_t>(N) * pre);
+    w.sbox = c.take<float4>(static_cast<size_t>(N) * pre);
+    w.sidx = c.take<int32_t>(static_cast<size_t>(N) * pre);
+    w.maskT = c.take<uint64_t>(static_cast<size_t>(N) * Wc * pre);
+    w.bytes = c.used();
+    return w;
+}
+
+// steps 2-6, shared by frcnn_propose and frcnn_nms
+static int sort_and_suppress(const ProposeWs& w, const float4* box_src, int N, int A, int pre,
+                             int post, double iou_thr, int out_mode, float4* out_rois,
+                             int32_t* out_idx, int64_t* out_keep, int32_t* out_count,
+                             hipStream_t st) {
+    const int Wc = (pre + 63) / 64;
+    hipLaunchKernelGGL(select_kernel, dim3(N), dim3(1024), 0, st, w.keys, A, pre, w.sel_T, w.sel_P,
+                       w.list_cnt);
+    FRCNN_LAUNCH_CHECK("select_kernel");
+    hipLaunchKernelGGL(compact_kernel, dim3((A + 255) / 256, N), dim3(256), 0, st, w.keys, A, pre,
+                       w.sel_T, w.list_cnt, w.list_keys);
+    FRCNN_LAUNCH_CHECK("compact_kernel");
+    hipLaunchKernelGGL(rank_kernel, dim3(Wc, N), dim3(256), 0, st, w.list_keys, pre, w.sel_P,
+                       box_src, A, w.sbox, w.sidx);
+    FRCNN_LAUNCH_CHECK("rank_kernel");
+    const NmsThr thr = make_thr(iou_thr);
+    const unsigned tiles = static_cast<unsigned>(Wc) * (Wc + 1) / 2;
+    hipLaunchKernelGGL(nms_mask_kernel, dim3(tiles, N), dim3(64), 0, st, w.sbox, pre, Wc, w.sel_P,
+                       thr, w.maskT);
+    FRCNN_LAUNCH_CHECK("nms_mask_kernel");
+    const size_t lds = static_cast<size_t>(Wc) * sizeof(uint64_t);
+    if (out_mode == 0)
+        hipLaunchKernelGGL(nms_sweep_kernel<0>, dim3(N), dim3(256), lds, st, w.maskT, w.sbox,
+                           w.sidx, pre, Wc, w.sel_P, post, out_rois, out_idx, out_keep, out_count);
+    else
+        hipLaunchKernelGGL(nms_sweep_kernel<1>, dim3(N), dim3(256), lds, st, w.maskT, w.sbox,
+                           w.sidx, pre, Wc, w.sel_P, post, out_rois, out_idx, out_keep, out_count);
+    FRCNN_LAUNCH_CHECK("nms_sweep_kernel");
+    return FRCNN_OK;
+}
+
+}  // namespace frcnn
+
+using namespace frcnn;
+
+static int check_params(const frcnn_propose_params* p) {
+    FRCNN_REQUIRE(p, "frcnn_propose: null params");
+    FRCNN_REQUIRE(p->N > 0 && p->N <= 65535, "frcnn_propose: N must be in [1, 65535]");
+    FRCNN_REQUIRE(p->A > 0, "frcnn_propose: A must be > 0");
+    FRCNN_REQUIRE(p->pre_nms > 0 && p->post_nms > 0, "frcnn_propose: pre/post_nms must be > 0");
+    FRCNN_REQUIRE(static_cast<int64_t>(p->pre_nms) <= (1 << 20), "frcnn_propose: pre_nms > 2^20");
+    return FRCNN_OK;
+}
+
+extern "C" size_t frcnn_propose_workspace_size(const frcnn_propose_params* p) {
+    if (check_params(p)) return 0;
+    const int pre = p->pre_nms < p->A ? p->pre_nms : p->A;
+    return carve(nullptr, p->N, p->A, pre, true).bytes;
+}
+
+extern "C" int frcnn_propose(const frcnn_propose_params* p, const float* scores, const float* deltas,
+                             const float* anchors, const float* anchor_base, float* out_rois,
+                             int32_t* out_idx, int32_t* out_count, void* workspace,
+                             size_t ws_bytes, void* stream) {
+    int rc = check_params(p);
+    if (rc) return rc;
+    FRCNN_REQUIRE(scores && deltas && out_rois && out_idx && out_count,
+                  "frcnn_propose: null pointer");
+    FRCNN_REQUIRE(anchors || anchor_base, "frcnn_propose: need anchors or anchor_base");
+    if (!anchors)
+        FRCNN_REQUIRE(p->K > 0 && p->feat_h > 0 && p->feat_w > 0 &&
+                          static_cast<int64_t>(p->K) * p->feat_h * p->feat_w == p->A,
+                      "frcnn_propose: A != feat_h*feat_w*K");
+    const int pre = p->pre_nms < p->A ? p->pre_nms : p->A;
+    ProposeWs w = carve(workspace, p->N, p->A, pre, true);
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_propose: workspace %zu < %zu",
+                  ws_bytes, w.bytes);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(decode_filter_kernel, dim3((p->A + 255) / 256, p->N), dim3(256), 0, st,
+                       scores, reinterpret_cast<const float4*>(deltas),
+                       reinterpret_cast<const float4*>(anchors),
+                       reinterpret_cast<const float4*>(anchor_base), p->A, p->K, p->feat_w,
+                       p->feat_stride, p->img_h, p->img_w, p->min_size, w.boxes, w.keys);
+    FRCNN_LAUNCH_CHECK("decode_filter_kernel");
+    return sort_and_suppress(w, w.boxes, p->N, p->A, pre, p->post_nms, p->iou_threshold, 0,
+                             reinterpret_cast<float4*>(out_rois), out_idx, nullptr, out_count, st);
+}
+
+extern "C" size_t frcnn_nms_workspace_size(int64_t n) {
+    if (n <= 0 || n > (1 << 20)) return 0;
+    return carve(nullptr, 1, static_cast<int>(n), static_cast<int>(n), false).bytes;
+}
+
+extern "C" int frcnn_nms(const float* boxes, const float* scores, int64_t n, double iou_threshold,
+                         int64_t* keep, int32_t* count, void* workspace, size_t ws_bytes,
+                         void* stream) {
+    FRCNN_REQUIRE(n >= 0 && n <= (1 << 20), "frcnn_nms: n must be in [0, 2^20]");
+    FRCNN_REQUIRE(count, "frcnn_nms: null count");
+    hipStream_t st = as_stream(stream);
+    if (n == 0) {
+        if (hipMemsetAsync(count, 0, sizeof(int32_t), st) != hipSuccess)
+            return check_launch("frcnn_nms memset");
+        return FRCNN_OK;
+    }
+    FRCNN_REQUIRE(boxes && scores && keep, "frcnn_nms: null pointer");
+    const int N = static_cast<int>(n);
+    ProposeWs w = carve(workspace, 1, N, N, false);
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_nms: workspace %zu < %zu", ws_bytes,
+                  w.bytes);
+    hipLaunchKernelGGL(nms_keys_kernel, dim3((N + 255) / 256), dim3(256), 0, st, scores, N, w.keys);
+    FRCNN_LAUNCH_CHECK("nms_keys_kernel");
+    return sort_and_suppress(w, reinterpret_cast<const float4*>(boxes), 1, N, N, N, iou_threshold,
+                             1, nullptr, nullptr, keep, count, st);
+}

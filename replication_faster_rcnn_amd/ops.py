@@ -1,0 +1,165 @@
+"""torchvision-surface ops the reference calls, on the HIP path.
+
+* ``nms(boxes, scores, iou_threshold)`` -- ``torchvision.ops.nms`` as called at
+  nets/rpn.py:75 (imported nets/rpn.py:4, utils/utils.py:4).
+* ``roi_pool(input, boxes, output_size, spatial_scale)`` -- ``torchvision.ops.
+  roi_pool`` as called at nets/heads.py:48, with an autograd backward (the
+  reference reaches torchvision's ``_roi_pool_backward`` from
+  ``total_loss.backward()`` at train.py:126).
+* ``propose(...)`` -- the batched proposal layer (nets/rpn.py:47-79 over all
+  images at once, replacing the per-image loop nets/rpn.py:131-136).
+
+Inputs may live on the CPU (reference style); they are moved to the current
+HIP device, and results are returned on the input's device.  Errors follow
+torchvision's ``TORCH_CHECK`` -> ``RuntimeError`` convention.
+"""
+from __future__ import annotations
+
+from typing import List, Tuple, Union
+
+import torch
+
+from . import _lib
+
+
+def _to_dev(t: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
+    return t.to(device=_lib.device(), dtype=dtype).contiguous()
+
+
+# ----------------------------------------------------------------------- nms
+def nms(boxes: torch.Tensor, scores: torch.Tensor, iou_threshold: float) -> torch.Tensor:
+    """torchvision.ops.nms: int64 indices of kept boxes, by decreasing score."""
+    lib = _lib.load()
+    if boxes.dim() != 2 or boxes.size(1) != 4:
+        raise RuntimeError(f"boxes should have 2 dimensions with 4 columns, got {tuple(boxes.shape)}")
+    if scores.dim() != 1 or scores.size(0) != boxes.size(0):
+        raise RuntimeError("boxes and scores should have the same number of elements in dim 0")
+    out_dev = boxes.device
+    b = _to_dev(boxes)
+    s = _to_dev(scores)
+    n = b.size(0)
+    keep = torch.empty(max(n, 1), dtype=torch.int64, device=b.device)
+    cnt = torch.zeros(1, dtype=torch.int32, device=b.device)
+    ws = _lib.workspace(lib.frcnn_nms_workspace_size(n), b.device)
+    _lib.check(lib.frcnn_nms(_lib.ptr(b), _lib.ptr(s), n, float(iou_threshold), _lib.ptr(keep),
+                             _lib.ptr(cnt), _lib.ptr(ws), ws.numel(), _lib.stream_ptr()), "nms")
+    k = int(cnt.item())
+    return keep[:k].to(out_dev)
+
+
+# ------------------------------------------------------------------ roi_pool
+def _roi_pool_fwd(x: torch.Tensor, rois: torch.Tensor, ph: int, pw: int, ss: float):
+    lib = _lib.load()
+    N, C, H, W = x.shape
+    R = rois.size(0)
+    out = torch.empty((R, C, ph, pw), dtype=torch.float32, device=x.device)
+    am = torch.empty((R, C, ph, pw), dtype=torch.int32, device=x.device)
+    _lib.check(lib.frcnn_roi_pool_fwd(_lib.ptr(x), _lib.ptr(rois), R, N, C, H, W, ph, pw, float(ss),
+                                      _lib.ptr(out), _lib.ptr(am), _lib.stream_ptr()),
+               "roi_pool forward")
+    return out, am
+
+
+def _roi_pool_bwd(grad: torch.Tensor, rois: torch.Tensor, am: torch.Tensor, shape, ss: float):
+    lib = _lib.load()
+    N, C, H, W = shape
+    R, _, ph, pw = grad.shape
+    gi = torch.empty((N, C, H, W), dtype=torch.float32, device=grad.device)
+    ws = _lib.workspace(lib.frcnn_roi_pool_bwd_workspace_size(R, N, ph, pw), grad.device)
+    _lib.check(lib.frcnn_roi_pool_bwd(_lib.ptr(grad), _lib.ptr(rois), _lib.ptr(am), R, N, C, H, W,
+                                      ph, pw, float(ss), _lib.ptr(gi), _lib.ptr(ws), ws.numel(),
+                                      _lib.stream_ptr()), "roi_pool backward")
+    return gi
+
+
+class _RoIPoolFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, rois, ph, pw, ss):
+        out, am = _roi_pool_fwd(x, rois, ph, pw, ss)
+        ctx.save_for_backward(rois, am)
+        ctx.meta = (tuple(x.shape), ss)
+        ctx.mark_non_differentiable(am)
+        return out, am
+
+    @staticmethod
+    def backward(ctx, grad_out, _grad_am):
+        rois, am = ctx.saved_tensors
+        shape, ss = ctx.meta
+        gi = _roi_pool_bwd(grad_out.contiguous().float(), rois, am, shape, ss)
+        return gi, None, None, None, None
+
+
+def _boxes_to_rois(boxes: Union[torch.Tensor, List[torch.Tensor]]) -> torch.Tensor:
+    if isinstance(boxes, (list, tuple)):  # torchvision's List[Tensor[L,4]] form
+        parts = [torch.cat([torch.full((b.size(0), 1), i, dtype=b.dtype, device=b.device), b], 1)
+                 for i, b in enumerate(boxes)]
+        boxes = torch.cat(parts, 0) if parts else torch.zeros((0, 5))
+    if boxes.dim() != 2 or boxes.size(1) != 5:
+        raise RuntimeError(f"boxes must be [K, 5] (batch_idx, x1, y1, x2, y2); got {tuple(boxes.shape)}")
+    return boxes
+
+
+def roi_pool_with_argmax(input: torch.Tensor, boxes, output_size, spatial_scale: float = 1.0
+                         ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """roi_pool returning (out, argmax int32) -- the torch.ops.torchvision.roi_pool pair."""
+    if input.dim() != 4:
+        raise RuntimeError("input must be [N, C, H, W]")
+    ph, pw = (output_size, output_size) if isinstance(output_size, int) else tuple(output_size)
+    out_dev = input.device
+    x = _to_dev(input)  # differentiable move, so CPU leaf tensors get their grad
+    rois = _to_dev(_boxes_to_rois(boxes))
+    out, am = _RoIPoolFunction.apply(x.contiguous(), rois, int(ph), int(pw), float(spatial_scale))
+    return out.to(out_dev), am.to(out_dev)
+
+
+def roi_pool(input: torch.Tensor, boxes, output_size, spatial_scale: float = 1.0) -> torch.Tensor:
+    """torchvision.ops.roi_pool (nets/heads.py:48)."""
+    return roi_pool_with_argmax(input, boxes, output_size, spatial_scale)[0]
+
+
+# ------------------------------------------------------------------ proposals
+def propose(scores: torch.Tensor, deltas: torch.Tensor, *, img_w: float, img_h: float,
+            pre_nms: int, post_nms: int, nms_thresh: float = 0.7, min_size: float = 16,
+            anchors: torch.Tensor = None, anchor_base: torch.Tensor = None, feat_h: int = 0,
+            feat_w: int = 0, feat_stride: int = 16):
+    """Batched proposal layer on device tensors.
+
+    scores fp32 [N, A], deltas fp32 [N, A, 4]; either explicit ``anchors``
+    [A, 4] or ``anchor_base`` [K, 4] + the feature grid (anchors generated in
+    the decode kernel).  Returns padded (rois [N, post, 4], anchor_idx int32
+    [N, post], count int32 [N]) -- no host synchronisation.
+    """
+    lib = _lib.load()
+    dev = scores.device
+    N, A = scores.shape
+    p = _lib.ProposeParams()
+    p.N, p.A = N, A
+    K = 0
+    if anchors is None:
+        K = anchor_base.size(0)
+        if K * feat_h * feat_w != A:
+            raise RuntimeError(f"A={A} != feat_h*feat_w*K={feat_h}*{feat_w}*{K}")
+    p.K, p.feat_h, p.feat_w, p.feat_stride = K, feat_h, feat_w, feat_stride
+    p.img_h, p.img_w, p.min_size = float(img_h), float(img_w), float(min_size)
+    p.pre_nms, p.post_nms, p.iou_threshold = int(pre_nms), int(post_nms), float(nms_thresh)
+    rois = torch.empty((N, post_nms, 4), dtype=torch.float32, device=dev)
+    idx = torch.empty((N, post_nms), dtype=torch.int32, device=dev)
+    cnt = torch.empty((N,), dtype=torch.int32, device=dev)
+    ws = _lib.workspace(lib.frcnn_propose_workspace_size(p), dev)
+    _lib.check(lib.frcnn_propose(p, _lib.ptr(scores), _lib.ptr(deltas), _lib.ptr(anchors),
+                                 _lib.ptr(anchor_base), _lib.ptr(rois), _lib.ptr(idx),
+                                 _lib.ptr(cnt), _lib.ptr(ws), ws.numel(), _lib.stream_ptr()),
+               "propose")
+    return rois, idx, cnt
+
+
+def roi_transform(rois: torch.Tensor, roi_inds: torch.Tensor, img_h, img_w, feat_h: int,
+                  feat_w: int) -> torch.Tensor:
+    """nets/heads.py:42-47 on device: [R,4] image rois + [R] inds -> [R,5]."""
+    lib = _lib.load()
+    R = rois.size(0)
+    out = torch.empty((R, 5), dtype=torch.float32, device=rois.device)
+    _lib.check(lib.frcnn_roi_transform(_lib.ptr(rois), _lib.ptr(roi_inds), R, float(img_h),
+                                       float(img_w), int(feat_h), int(feat_w), _lib.ptr(out),
+                                       _lib.stream_ptr()), "roi_transform")
+    return out

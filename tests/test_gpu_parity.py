@@ -1,0 +1,186 @@
+"""HIP path vs oracle / golden fixtures.  Needs an MI355X.
+
+Bars (BASELINE.json north_star): kept-proposal indices, RoIPool outputs and
+argmax bit-exact; decoded boxes within 1e-5 relative (fp32 exp is
+host-dependent in the reference); RoIPool gradients bit-exact here (the
+kernel reproduces the CPU summation order), 1e-5 relative is the contract.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_numpy as orc
+from replication_faster_rcnn_amd import anchors as A
+from replication_faster_rcnn_amd import ops, synth
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+RTOL = 1e-5
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def test_anchor_base_and_grid(golden):
+    g = golden("anchors.npz")
+    for tag, scales in [("k9", (8, 16, 32)), ("k15", (2, 4, 8, 16, 32))]:
+        base = A.generate_anchor_base(anchor_scales=list(scales))
+        assert np.array_equal(base, g[f"base_{tag}"]), tag
+        for (w, h) in [(10, 10), (63, 38), (38, 38), (84, 50), (7, 3)]:
+            a = A.generate_anchors(base, 16, w, h)
+            assert a.dtype == np.float32
+            assert sha(a) == str(g[f"sha_{tag}_{w}x{h}"]), (tag, w, h)
+    a10 = A.generate_anchors(A.generate_anchor_base(), 10, 10, 10)
+    assert np.array_equal(a10, g["anchors_main_10"])
+
+
+def test_reg2bbox(golden):
+    from replication_faster_rcnn_amd import utils as U
+    g = golden("reg2bbox.npz")
+    out = U.reg2bbox(torch.from_numpy(g["anchors"]), torch.from_numpy(g["reg"])).numpy()
+    ora = orc.reg2bbox(g["anchors"], g["reg"])
+    fin = np.isfinite(ora)
+    assert np.array_equal(np.isfinite(out), fin)
+    assert np.array_equal(out[fin], ora[fin])           # both correctly rounded
+    np.testing.assert_allclose(out[fin], g["out"][fin], rtol=RTOL, atol=1e-3)  # vs MKL exp
+
+
+def _propose_one_gpu(anchors, scores, deltas, img_w, img_h, pre, post):
+    rois, idx, cnt = ops.propose(torch.from_numpy(scores)[None].to(DEV),
+                                 torch.from_numpy(deltas)[None].to(DEV), img_w=img_w, img_h=img_h,
+                                 pre_nms=pre, post_nms=post,
+                                 anchors=torch.from_numpy(anchors).to(DEV))
+    k = int(cnt[0])
+    return rois[0, :k].cpu().numpy(), idx[0, :k].cpu().numpy().astype(np.int64)
+
+
+@pytest.mark.parametrize("case", [0, 1, 2])
+def test_propose_small_vs_reference(golden, case):
+    g = golden(f"proposal_small{case}.npz")
+    anchors = orc.generate_anchors(orc.generate_anchor_base(), 16, int(g["feat_w"]), int(g["feat_h"]))
+    rois, idx = _propose_one_gpu(anchors, g["scores"], g["deltas"], int(g["img_w"]), int(g["img_h"]),
+                                 int(g["pre"]), int(g["post"]))
+    assert np.array_equal(idx, g["idx"])
+    np.testing.assert_allclose(rois, g["rois"], rtol=RTOL, atol=1e-4)
+    # and bit-exact against the oracle (same correctly-rounded exp)
+    orois, oidx = orc.propose_one(anchors, g["scores"], g["deltas"], int(g["img_w"]),
+                                  int(g["img_h"]), int(g["pre"]), int(g["post"]))
+    assert np.array_equal(rois, orois)
+
+
+@pytest.mark.parametrize("cfg,imgs", [("cfg1", (0, 1)), ("cfg2", (0, 1, 2, 3)), ("cfg4", (0,)),
+                                      ("cfg5", (0, 1))])
+def test_propose_batched_full_size(golden, cfg, imgs):
+    """Batched path with in-kernel anchors at the BASELINE shapes."""
+    g = golden("proposal_full.npz")
+    c = synth.CONFIGS[cfg]
+    base = A.generate_anchor_base_device(anchor_scales=c["scales"])
+    K = base.size(0)
+    Anc = c["feat_h"] * c["feat_w"] * K
+    sc = torch.from_numpy(np.stack([synth.rpn_scores(Anc, 0, i) for i in imgs])).to(DEV)
+    de = torch.from_numpy(np.stack([synth.rpn_deltas(Anc, 0, i) for i in imgs])).to(DEV)
+    rois, idx, cnt = ops.propose(sc, de, img_w=c["img_w"], img_h=c["img_h"], pre_nms=c["pre_nms"],
+                                 post_nms=c["post_nms"], anchor_base=base, feat_h=c["feat_h"],
+                                 feat_w=c["feat_w"])
+    for j, i in enumerate(imgs):
+        k = int(cnt[j])
+        gi = g[f"{cfg}_img{i}_idx"]
+        assert k == len(gi)
+        assert np.array_equal(idx[j, :k].cpu().numpy().astype(np.int64), gi), (cfg, i)
+        np.testing.assert_allclose(rois[j, :k].cpu().numpy(), g[f"{cfg}_img{i}_rois"], rtol=RTOL,
+                                   atol=1e-4)
+        assert (idx[j, k:] == -1).all()
+
+
+def test_propose_batch_invariance():
+    """P-invariance: an image's proposals do not depend on its batch mates."""
+    c = synth.CONFIGS["cfg2"]
+    base = A.generate_anchor_base_device()
+    Anc = c["feat_h"] * c["feat_w"] * 9
+    sc = torch.from_numpy(np.stack([synth.rpn_scores(Anc, 5, i) for i in range(6)])).to(DEV)
+    de = torch.from_numpy(np.stack([synth.rpn_deltas(Anc, 5, i) for i in range(6)])).to(DEV)
+    kw = dict(img_w=c["img_w"], img_h=c["img_h"], pre_nms=c["pre_nms"], post_nms=c["post_nms"],
+              anchor_base=base, feat_h=c["feat_h"], feat_w=c["feat_w"])
+    full = ops.propose(sc, de, **kw)
+    part = ops.propose(sc[3:5], de[3:5], **kw)
+    for a, b in zip(full, part):
+        assert torch.equal(a[3:5], b)
+
+
+def test_nms_fixtures(golden):
+    g = golden("nms.npz")
+    names = sorted({k.rsplit("_", 1)[0] for k in g if k.endswith("_keep")})
+    for n in names:
+        keep = ops.nms(torch.from_numpy(g[f"{n}_boxes"]), torch.from_numpy(g[f"{n}_scores"]),
+                       float(g[f"{n}_thr"]))
+        assert keep.dtype == torch.int64
+        assert np.array_equal(keep.numpy(), g[f"{n}_keep"]), n
+
+
+def test_nms_random_thresholds():
+    r = np.random.default_rng(3)
+    for n, thr in [(1, 0.5), (63, 0.7), (64, 0.7), (65, 0.3), (1000, 0.9), (4097, 0.7)]:
+        xy = r.uniform(0, 100, (n, 2)).astype(np.float32)
+        wh = r.uniform(1, 40, (n, 2)).astype(np.float32)
+        b = np.concatenate([xy, xy + wh], 1)
+        s = r.random(n).astype(np.float32)
+        keep = ops.nms(torch.from_numpy(b), torch.from_numpy(s), thr).numpy()
+        assert np.array_equal(keep, orc.nms(b, s, thr)), (n, thr)
+    empty = ops.nms(torch.zeros((0, 4)), torch.zeros(0), 0.7)
+    assert empty.numel() == 0
+
+
+def test_roi_pool_golden(golden):
+    g = golden("roi_pool.npz")
+    x = torch.from_numpy(g["x"]).to(DEV)
+    rois = torch.from_numpy(g["rois_img"]).to(DEV)
+    inds = torch.from_numpy(g["roi_inds"]).to(DEV)
+    boxes = ops.roi_transform(rois, inds, int(g["img_h"]), int(g["img_w"]), x.shape[2], x.shape[3])
+    assert np.array_equal(boxes.cpu().numpy(), g["boxes"])
+    xg = x.clone().requires_grad_(True)
+    out, am = ops.roi_pool_with_argmax(xg, boxes, (7, 7), 1.0)
+    assert np.array_equal(out.detach().cpu().numpy(), g["out"])
+    assert np.array_equal(am.cpu().numpy(), g["argmax"])
+    out.backward(torch.from_numpy(g["grad"]).to(DEV))
+    gi = xg.grad.cpu().numpy()
+    np.testing.assert_allclose(gi, g["grad_in"], rtol=RTOL, atol=1e-6)
+    assert np.array_equal(gi, g["grad_in"])  # CPU summation order reproduced
+
+
+@pytest.mark.parametrize("N,C,H,W,R,ph", [(8, 256, 38, 63, 2400, 7), (2, 3, 9, 11, 77, 3),
+                                          (1, 5, 4, 4, 40, 7), (2, 64, 50, 84, 300, 7)])
+def test_roi_pool_vs_oracle(N, C, H, W, R, ph):
+    r = np.random.default_rng(R)
+    x = r.standard_normal((N, C, H, W), dtype=np.float32)
+    x[:, :, ::3, ::2] = x[:, :, ::3, 1::2].max()  # ties: first max must win
+    b = r.integers(0, N, R).astype(np.float32)
+    xy = r.uniform(-3, max(H, W) + 2, (R, 2)).astype(np.float32)
+    wh = r.uniform(-2, max(H, W), (R, 2)).astype(np.float32)
+    rois = np.concatenate([b[:, None], xy, xy + wh], 1).astype(np.float32)
+    out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV),
+                                       ph, 1.0)
+    oo, oa = orc.roi_pool_forward(x, rois, ph, 1.0)
+    assert np.array_equal(out.cpu().numpy(), oo)
+    assert np.array_equal(am.cpu().numpy(), oa)
+    gr = r.standard_normal(oo.shape).astype(np.float32)
+    from replication_faster_rcnn_amd.ops import _roi_pool_bwd
+    gi = _roi_pool_bwd(torch.from_numpy(gr).to(DEV), torch.from_numpy(rois).to(DEV), am, x.shape, 1.0)
+    ref = orc.roi_pool_backward(gr, rois, oa, x.shape)
+    np.testing.assert_allclose(gi.cpu().numpy(), ref, rtol=RTOL, atol=1e-6)
+    assert np.array_equal(gi.cpu().numpy(), ref)
+
+
+def test_roi_pool_bwd_deterministic():
+    r = np.random.default_rng(1)
+    x = torch.from_numpy(r.standard_normal((2, 16, 20, 20), dtype=np.float32)).to(DEV)
+    rois = torch.tensor([[0, 0, 0, 19, 19], [1, 2, 2, 3, 3], [0, 5, 5, 5.4, 5.4]] * 30,
+                        dtype=torch.float32, device=DEV)
+    out, am = ops.roi_pool_with_argmax(x, rois, 7)
+    g = torch.randn(out.shape, device=DEV)
+    from replication_faster_rcnn_amd.ops import _roi_pool_bwd
+    a = _roi_pool_bwd(g, rois, am, x.shape, 1.0)
+    b = _roi_pool_bwd(g, rois, am, x.shape, 1.0)
+    assert torch.equal(a, b)
