@@ -81,7 +81,8 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
 __device__ __forceinline__ uint32_t desc_score_key(float s) {
     uint32_t u = __float_as_uint(s);
     uint32_t asc = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-    return ~asc;
+    uint32_t k = ~asc;
+    return k == 0xFFFFFFFFu ? 0xFFFFFFFEu : k;  // 0xFFFFFFFF is reserved for "invalid"
 }
 
 // torch.clamp(v, lo, hi) on fp32 with NaN propagation (nets/rpn.py:62-63).

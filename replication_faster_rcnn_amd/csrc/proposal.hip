@@ -18,6 +18,7 @@
 // the reference's CPU argsort is unstable under ties).
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "common.h"
@@ -384,6 +385,294 @@ __global__ __launch_bounds__(256) void nms_sweep_kernel(
     if (tid == 0) out_count[n] = count;
 }
 
+// ==================================================== fused per-image path
+// One 1024-thread workgroup per image does select -> sort -> NMS with all
+// working state on chip:
+//   * the image's score keys live in registers (KPT per lane, anchor index
+//     implied by the slot: a = tid + k*1024);
+//   * the next CHUNK(=1024) candidates in rank order are found with an exact
+//     radix select (12/12/8-bit digits, LDS histograms), compacted into LDS and
+//     bitonic-sorted (shuffles below 64, LDS above);
+//   * NMS is lazy: each block of 64 sorted candidates is tested only against
+//     the boxes kept so far (16 waves split the kept list) and against itself
+//     (64x64 tile), then resolved by a wave with a fixed-point iteration
+//     (K <- avail & ~OR_{i in K} D[i]); it stops as soon as post_nms are kept.
+// Work is O(rows_examined x kept), not O(pre_nms^2).
+constexpr int kChunk = 1024;
+constexpr int kHistBins = 4096;
+constexpr int kFusedMaxA = 24 * 1024;  // keys held in registers: <= 24 per lane
+
+struct FusedShared {
+    unsigned digit, before, bucket;
+    unsigned ccount;
+    int kcount;
+    unsigned wsum[16];
+    uint64_t red[16];
+    uint64_t diag[64];
+};
+
+// Block-wide: find the bin d with cum(bins < d) < need <= cum(bins <= d).
+__device__ __forceinline__ void hist_find(const unsigned* hist, int nbins, unsigned need,
+                                          FusedShared& sh) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    unsigned h[4], loc = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        int bi = 4 * tid + q;
+        h[q] = bi < nbins ? hist[bi] : 0u;
+        loc += h[q];
+    }
+    unsigned incl = loc;
+    for (int o = 1; o < 64; o <<= 1) {
+        unsigned v = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += v;
+    }
+    if (lane == 63) sh.wsum[wid] = incl;
+    __syncthreads();
+    unsigned before = incl - loc;
+    for (int w = 0; w < wid; ++w) before += sh.wsum[w];
+    if (before < need && before + loc >= need) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (before < need && before + h[q] >= need) {
+                sh.digit = 4 * tid + q;
+                sh.before = before;
+                sh.bucket = h[q];
+            }
+            before += h[q];
+        }
+    }
+    __syncthreads();
+}
+
+// r-th smallest (1-based) valid key64 = (score_key << 32 | anchor index).
+template <int KPT>
+__device__ uint64_t select_rank(const uint32_t (&sk)[KPT], int A, unsigned r, unsigned* hist,
+                                FusedShared& sh) {
+    const int tid = threadIdx.x;
+    uint64_t prefix = 0;
+    unsigned need = r;
+    int done = 0;
+#pragma unroll 1
+    for (int pass = 0; pass < 6; ++pass) {
+        const int width = (pass % 3 == 2) ? 8 : 12;
+        const int shift = 64 - done - width;
+        const int nbins = 1 << width;
+        for (int i = tid; i < nbins; i += 1024) hist[i] = 0;
+        __syncthreads();
+        const uint64_t hm = done == 0 ? 0ull : (~0ull << (64 - done));
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) {
+            const int a = tid + k * 1024;
+            if (a < A && sk[k] != 0xFFFFFFFFu) {
+                const uint64_t key = (static_cast<uint64_t>(sk[k]) << 32) | static_cast<uint32_t>(a);
+                if ((key & hm) == prefix)
+                    atomicAdd(&hist[static_cast<unsigned>(key >> shift) & (nbins - 1)], 1u);
+            }
+        }
+        __syncthreads();
+        hist_find(hist, nbins, need, sh);
+        const unsigned d = sh.digit;
+        need -= sh.before;
+        prefix |= static_cast<uint64_t>(d) << shift;
+        done += width;
+        const bool whole = sh.bucket == need;
+        __syncthreads();  // sh.* consumed before the next pass rewrites them
+        if (whole) return prefix | ((1ull << shift) - 1ull);
+    }
+    return prefix;
+}
+
+template <int KPT>
+__global__ __launch_bounds__(1024) void propose_fused_kernel(
+    const uint64_t* __restrict__ keys_all, const float4* __restrict__ boxes_all, int A, int pre,
+    int post, NmsThr thr, float4* __restrict__ out_rois, int32_t* __restrict__ out_idx,
+    int32_t* __restrict__ out_count) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    __shared__ FusedShared sh;
+    unsigned* hist = reinterpret_cast<unsigned*>(lds_raw);                          // 16 KB
+    uint64_t* ckey = reinterpret_cast<uint64_t*>(lds_raw + kHistBins * 4);          //  8 KB
+    float4* cbox = reinterpret_cast<float4*>(lds_raw + kHistBins * 4 + kChunk * 8); // 16 KB
+    float* carea = reinterpret_cast<float*>(lds_raw + kHistBins * 4 + kChunk * 24); //  4 KB
+    float4* kbox = reinterpret_cast<float4*>(lds_raw + kHistBins * 4 + kChunk * 28);
+    float* karea = reinterpret_cast<float*>(lds_raw + kHistBins * 4 + kChunk * 28 + post * 16);
+
+    const int n = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t* keys = keys_all + static_cast<size_t>(n) * A;
+    const float4* boxes = boxes_all + static_cast<size_t>(n) * A;
+    float4* orois = out_rois + static_cast<size_t>(n) * post;
+    int32_t* oidx = out_idx + static_cast<size_t>(n) * post;
+
+    uint32_t sk[KPT];
+    unsigned nv = 0;
+#pragma unroll
+    for (int k = 0; k < KPT; ++k) {
+        const int a = tid + k * 1024;
+        const uint64_t key = a < A ? keys[a] : kInvalidKey;
+        sk[k] = key == kInvalidKey ? 0xFFFFFFFFu : static_cast<uint32_t>(key >> 32);
+        nv += sk[k] != 0xFFFFFFFFu;
+    }
+    nv = wave_sum_u32(nv);
+    if (lane == 0) sh.wsum[wid] = nv;
+    if (tid == 0) sh.kcount = 0;
+    __syncthreads();
+    unsigned M = 0;
+    for (int w = 0; w < 16; ++w) M += sh.wsum[w];
+    const int P = static_cast<int>(M < static_cast<unsigned>(pre) ? M : static_cast<unsigned>(pre));
+    __syncthreads();
+
+    int r_done = 0;
+    uint64_t T_prev = 0;
+    bool have_prev = false;
+    int kcount = 0;
+    while (r_done < P && kcount < post) {
+        const int r_end = min(r_done + kChunk, P);
+        const uint64_t T = select_rank<KPT>(sk, A, static_cast<unsigned>(r_end), hist, sh);
+        if (tid == 0) sh.ccount = 0;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) {
+            const int a = tid + k * 1024;
+            if (a < A && sk[k] != 0xFFFFFFFFu) {
+                const uint64_t key = (static_cast<uint64_t>(sk[k]) << 32) | static_cast<uint32_t>(a);
+                if (key <= T && (!have_prev || key > T_prev)) ckey[atomicAdd(&sh.ccount, 1u)] = key;
+            }
+        }
+        __syncthreads();
+        const int cc = r_end - r_done;  // == sh.ccount (keys are unique)
+        // ---- bitonic sort of the chunk, ascending
+        uint64_t key = tid < cc ? ckey[tid] : kInvalidKey;
+#pragma unroll 1
+        for (int kk = 2; kk <= kChunk; kk <<= 1) {
+#pragma unroll 1
+            for (int j = kk >> 1; j > 0; j >>= 1) {
+                uint64_t other;
+                if (j >= 64) {
+                    __syncthreads();
+                    ckey[tid] = key;
+                    __syncthreads();
+                    other = ckey[tid ^ j];
+                } else {
+                    other = __shfl_xor(key, j, 64);
+                }
+                const bool asc = (tid & kk) == 0;
+                const bool lower = (tid & j) == 0;
+                const uint64_t mn = other < key ? other : key;
+                const uint64_t mx = other < key ? key : other;
+                key = (lower == asc) ? mn : mx;
+            }
+        }
+        __syncthreads();
+        ckey[tid] = key;
+        if (tid < cc) {
+            const float4 b = boxes[static_cast<uint32_t>(key)];
+            cbox[tid] = b;
+            carea[tid] = box_area(b);
+        }
+        __syncthreads();
+        // ---- lazy NMS over 64-candidate blocks
+        const int nb = (cc + 63) / 64;
+#pragma unroll 1
+        for (int blk = 0; blk < nb && kcount < post; ++blk) {
+            const int j = blk * 64 + lane;
+            const bool jv = j < cc;
+            float4 bj = make_float4(0.f, 0.f, 0.f, 0.f);
+            float aj = 0.f;
+            if (jv) {
+                bj = cbox[j];
+                aj = carea[j];
+            }
+            bool sup = false;
+            if (jv && !thr.never)
+                for (int i = wid; i < kcount; i += 16)
+                    if (iou_over(kbox[i], karea[i], bj, aj, thr)) {
+                        sup = true;
+                        break;
+                    }
+            const uint64_t supm = __ballot(sup);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int r = wid + 16 * q;
+                const int ia = blk * 64 + r;
+                bool bit = false;
+                if (jv && lane > r && ia < cc && !thr.never) bit = iou_over(cbox[ia], carea[ia], bj, aj, thr);
+                const uint64_t D = __ballot(bit);
+                if (lane == 0) sh.diag[r] = D;
+            }
+            if (lane == 0) sh.red[wid] = supm;
+            __syncthreads();
+            if (wid == 0) {
+                uint64_t removed = 0;
+                for (int w = 0; w < 16; ++w) removed |= sh.red[w];
+                const int rows = cc - blk * 64;
+                if (rows < 64) removed |= ~0ull << rows;
+                const uint64_t avail = ~removed;
+                const uint64_t Dl = sh.diag[lane];
+                uint64_t K = avail;
+#pragma unroll 1
+                for (int it = 0; it < 65; ++it) {  // fixed point (<= 64 iterations)
+                    const uint64_t rb = wave_or_u64(((K >> lane) & 1ull) ? Dl : 0ull);
+                    const uint64_t Kn = avail & ~rb;
+                    if (Kn == K) break;
+                    K = Kn;
+                }
+                int room = post - kcount;
+                while (__popcll(K) > room) K &= ~(1ull << (63 - __clzll(K)));  // keep the first `room`
+                if ((K >> lane) & 1ull) {
+                    const int slot = kcount + __popcll(K & lanemask_lt());
+                    kbox[slot] = bj;
+                    karea[slot] = aj;
+                    orois[slot] = bj;
+                    oidx[slot] = static_cast<int32_t>(static_cast<uint32_t>(ckey[j]));
+                }
+                if (lane == 0) sh.kcount = kcount + __popcll(K);
+            }
+            __syncthreads();
+            kcount = sh.kcount;
+        }
+        r_done = r_end;
+        T_prev = T;
+        have_prev = true;
+    }
+    for (int s = kcount + tid; s < post; s += 1024) {
+        orois[s] = make_float4(0.f, 0.f, 0.f, 0.f);
+        oidx[s] = -1;
+    }
+    if (tid == 0) out_count[n] = kcount;
+}
+
+static size_t fused_lds_bytes(int post) {
+    return static_cast<size_t>(kHistBins) * 4 + kChunk * 28 + static_cast<size_t>(post) * 20;
+}
+
+static int launch_fused(const uint64_t* keys, const float4* boxes, int N, int A, int pre, int post,
+                        const NmsThr& thr, float4* out_rois, int32_t* out_idx, int32_t* out_count,
+                        hipStream_t st) {
+    const size_t lds = fused_lds_bytes(post);
+    const int kpt = (A + 1023) / 1024;
+#define FRCNN_FUSED(KP)                                                                         \
+    hipLaunchKernelGGL(propose_fused_kernel<KP>, dim3(N), dim3(1024), lds, st, keys, boxes, A, pre, \
+                       post, thr, out_rois, out_idx, out_count)
+    if (kpt <= 8) FRCNN_FUSED(8);
+    else if (kpt <= 16) FRCNN_FUSED(16);
+    else FRCNN_FUSED(24);
+#undef FRCNN_FUSED
+    FRCNN_LAUNCH_CHECK("propose_fused_kernel");
+    return FRCNN_OK;
+}
+
+// Which proposal path: the fused per-image kernel fills one CU per image and
+// does O(rows x kept) IoU work; the wide path spreads an O(pre^2/2) bitmask
+// over the whole chip.  Few images with a large post_nms -> wide.
+static bool use_fused(int N, int A, int post) {
+    const char* force = getenv("FRCNN_PROPOSE_PATH");  // test / bench override
+    if (A > kFusedMaxA || post > 4096) return false;
+    if (force && force[0] == 'f') return true;
+    if (force && force[0] == 'w') return false;
+    return N >= 4 || post <= 1000;
+}
+
 // ------------------------------------------------------------ workspace map
 struct ProposeWs {
     uint64_t* keys;
@@ -489,6 +778,9 @@ extern "C" int frcnn_propose(const frcnn_propose_params* p, const float* scores,
                        reinterpret_cast<const float4*>(anchor_base), p->A, p->K, p->feat_w,
                        p->feat_stride, p->img_h, p->img_w, p->min_size, w.boxes, w.keys);
     FRCNN_LAUNCH_CHECK("decode_filter_kernel");
+    if (use_fused(p->N, p->A, p->post_nms))
+        return launch_fused(w.keys, w.boxes, p->N, p->A, pre, p->post_nms, make_thr(p->iou_threshold),
+                            reinterpret_cast<float4*>(out_rois), out_idx, out_count, st);
     return sort_and_suppress(w, w.boxes, p->N, p->A, pre, p->post_nms, p->iou_threshold, 0,
                              reinterpret_cast<float4*>(out_rois), out_idx, nullptr, out_count, st);
 }

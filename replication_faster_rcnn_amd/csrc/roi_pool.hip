@@ -17,6 +17,8 @@
 // exactly the CPU order n -> ph -> pw.  The finished planes are stored once
 // (zero-fill of grad_in fused).
 #include <cfloat>
+#include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 
@@ -119,6 +121,215 @@ __global__ __launch_bounds__(256) void roi_pool_fwd_kernel(const float* __restri
     }
 }
 
+// Image-tile forward: a workgroup owns CG channel planes of image b (staged in
+// LDS with one coalesced pass over HBM) and produces every RoI of that image
+// (its share `split` of them) for those channels.  Outputs of one RoI for the
+// CG channels are CG*PH*PW contiguous floats, written 4 per lane (float4 +
+// int4).  Bin geometry is recomputed per element from 4 RoI scalars in LDS.
+struct RoiGeom {
+    int sh, sw;
+    float bh, bw;
+};
+
+__device__ __forceinline__ RoiGeom roi_geom(const float* roi, float ss, int PH, int PW) {
+    int sw = static_cast<int>(roundf(roi[1] * ss));
+    int sh = static_cast<int>(roundf(roi[2] * ss));
+    int ew = static_cast<int>(roundf(roi[3] * ss));
+    int eh = static_cast<int>(roundf(roi[4] * ss));
+    int rw = ew - sw + 1;
+    int rh = eh - sh + 1;
+    rw = rw > 1 ? rw : 1;
+    rh = rh > 1 ? rh : 1;
+    RoiGeom g;
+    g.sh = sh;
+    g.sw = sw;
+    g.bh = static_cast<float>(rh) / static_cast<float>(PH);
+    g.bw = static_cast<float>(rw) / static_cast<float>(PW);
+    return g;
+}
+
+__device__ __forceinline__ int4 geom_bin(const RoiGeom& g, int H, int W, int ph, int pw) {
+    int hs = static_cast<int>(floorf(static_cast<float>(ph) * g.bh)) + g.sh;
+    int ws = static_cast<int>(floorf(static_cast<float>(pw) * g.bw)) + g.sw;
+    int he = static_cast<int>(ceilf(static_cast<float>(ph + 1) * g.bh)) + g.sh;
+    int we = static_cast<int>(ceilf(static_cast<float>(pw + 1) * g.bw)) + g.sw;
+    return make_int4(min(max(hs, 0), H), min(max(he, 0), H), min(max(ws, 0), W),
+                     min(max(we, 0), W));
+}
+
+constexpr int kTileRois = 64;   // RoI geometry staged per batch
+constexpr int kTileThreads = 512;
+
+// Four bin windows scanned in lock-step (4 independent LDS chains per lane).
+// Each window keeps torchvision's row-major scan with a strict '>' update, so
+// the result (max, first index of the max) is exactly the CPU kernel's.
+__device__ __forceinline__ void pool_window4(const float* const (&pl)[4], int W, const int4 (&g)[4],
+                                             float (&mv)[4], int (&mi)[4]) {
+    int hmax = 0, wmax = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        mv[q] = (g[q].y <= g[q].x || g[q].w <= g[q].z) ? 0.0f : -FLT_MAX;
+        mi[q] = -1;
+        hmax = max(hmax, g[q].y - g[q].x);
+        wmax = max(wmax, g[q].w - g[q].z);
+    }
+    for (int dh = 0; dh < hmax; ++dh) {
+        for (int dw = 0; dw < wmax; ++dw) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int h = g[q].x + dh, w = g[q].z + dw;
+                if (h < g[q].y && w < g[q].w) {
+                    const int ii = h * W + w;
+                    const float v = pl[q][ii];
+                    if (v > mv[q]) {
+                        mv[q] = v;
+                        mi[q] = ii;
+                    }
+                }
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kTileThreads) void roi_pool_fwd_tile_kernel(
+    const float* __restrict__ x, const float* __restrict__ rois, const int* __restrict__ list,
+    const int* __restrict__ cnt, int R, int C, int H, int W, int PH, int PW, int CG, float ss,
+    float* __restrict__ out, int32_t* __restrict__ argmax) {
+    extern __shared__ __attribute__((aligned(16))) float planes[];  // [CG][H*W]
+    __shared__ RoiGeom geo[kTileRois];
+    __shared__ int rid[kTileRois];
+    const int b = blockIdx.y;
+    const int c0 = blockIdx.x * CG;
+    const int tid = threadIdx.x;
+    const int HW = H * W;
+    const int PHW = PH * PW;
+    const int nr = cnt[b];
+    const int split = gridDim.z;
+    const int r_begin = static_cast<int>(static_cast<int64_t>(nr) * blockIdx.z / split);
+    const int r_end = static_cast<int>(static_cast<int64_t>(nr) * (blockIdx.z + 1) / split);
+    if (r_begin >= r_end) return;
+    // stage the CG planes (contiguous in NCHW): float4 when aligned
+    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+    const int nf = CG * HW;
+    if ((nf & 3) == 0 && ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        float4* d4 = reinterpret_cast<float4*>(planes);
+        for (int i = tid; i < nf / 4; i += kTileThreads) d4[i] = s4[i];
+    } else {
+        for (int i = tid; i < nf; i += kTileThreads) planes[i] = src[i];
+    }
+    const int per_roi = CG * PHW;  // multiple of 4 (CG % 4 == 0)
+    const int* lst = list + static_cast<size_t>(b) * R;
+    for (int t0 = r_begin; t0 < r_end; t0 += kTileRois) {
+        const int nt = min(kTileRois, r_end - t0);
+        __syncthreads();  // planes staged / previous batch's geometry consumed
+        if (tid < nt) {
+            int r = lst[t0 + tid];
+            rid[tid] = r;
+            geo[tid] = roi_geom(rois + static_cast<size_t>(r) * 5, ss, PH, PW);
+        }
+        __syncthreads();
+        const int total = nt * per_roi;
+        for (int f0 = tid * 4; f0 < total; f0 += 4 * kTileThreads) {
+            // f0..f0+3 lie in one RoI's contiguous run (per_roi % 4 == 0)
+            const int t = f0 / per_roi;
+            const int e = f0 - t * per_roi;
+            int cl = e / PHW;
+            int k = e - cl * PHW;
+            const RoiGeom gm = geo[t];
+            const float* pl[4];
+            int4 g[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                g[q] = geom_bin(gm, H, W, k / PW, k % PW);
+                pl[q] = planes + cl * HW;
+                if (++k == PHW) {
+                    k = 0;
+                    ++cl;
+                }
+            }
+            float v[4];
+            int m[4];
+            pool_window4(pl, W, g, v, m);
+            const size_t o = static_cast<size_t>(rid[t]) * C * PHW + static_cast<size_t>(c0) * PHW + e;
+            *reinterpret_cast<float4*>(out + o) = make_float4(v[0], v[1], v[2], v[3]);
+            *reinterpret_cast<int4*>(argmax + o) = make_int4(m[0], m[1], m[2], m[3]);
+        }
+    }
+}
+
+// Wave-per-RoI variant: lane = bin (PH*PW <= 64), each lane pools its bin
+// window in CG channel planes at once -- one loop control, CG independent LDS
+// chains (plane offsets are immediates).  A wave writes one RoI's CG channel
+// rows: out[r][c0+q][0..PHW) are PHW consecutive floats per q.
+template <int CG>
+__global__ __launch_bounds__(kTileThreads) void roi_pool_fwd_wave_kernel(
+    const float* __restrict__ x, const float* __restrict__ rois, const int* __restrict__ list,
+    const int* __restrict__ cnt, int R, int C, int H, int W, int PH, int PW, float ss,
+    float* __restrict__ out, int32_t* __restrict__ argmax) {
+    extern __shared__ __attribute__((aligned(16))) float planes[];  // [CG][H*W]
+    const int b = blockIdx.y;
+    const int c0 = blockIdx.x * CG;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    constexpr int kWaves = kTileThreads / 64;
+    const int HW = H * W;
+    const int PHW = PH * PW;
+    const int nr = cnt[b];
+    const int split = gridDim.z;
+    const int r_begin = static_cast<int>(static_cast<int64_t>(nr) * blockIdx.z / split);
+    const int r_end = static_cast<int>(static_cast<int64_t>(nr) * (blockIdx.z + 1) / split);
+    if (r_begin >= r_end) return;
+    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+    const int nf = CG * HW;
+    if ((nf & 3) == 0 && ((reinterpret_cast<uintptr_t>(src) & 15) == 0)) {
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        float4* d4 = reinterpret_cast<float4*>(planes);
+        for (int i = tid; i < nf / 4; i += kTileThreads) d4[i] = s4[i];
+    } else {
+        for (int i = tid; i < nf; i += kTileThreads) planes[i] = src[i];
+    }
+    __syncthreads();
+    const int* lst = list + static_cast<size_t>(b) * R;
+    const int ph = lane / PW, pw = lane - (lane / PW) * PW;
+    const bool act = lane < PHW;
+    for (int t = r_begin + wid; t < r_end; t += kWaves) {
+        const int r = __builtin_amdgcn_readfirstlane(lst[t]);
+        const RoiGeom gm = roi_geom(rois + static_cast<size_t>(r) * 5, ss, PH, PW);
+        int4 g = geom_bin(gm, H, W, ph, pw);
+        if (!act) g = make_int4(0, 0, 0, 0);
+        const bool empty = g.y <= g.x || g.w <= g.z;
+        float mv[CG];
+        int mi[CG];
+#pragma unroll
+        for (int q = 0; q < CG; ++q) {
+            mv[q] = empty ? 0.0f : -FLT_MAX;
+            mi[q] = -1;
+        }
+        for (int h = g.x; h < g.y; ++h) {
+            const float* row = planes + h * W;
+            for (int w = g.z; w < g.w; ++w) {
+                const int ii = h * W + w;
+#pragma unroll
+                for (int q = 0; q < CG; ++q) {
+                    const float v = row[q * HW + w];
+                    if (v > mv[q]) {
+                        mv[q] = v;
+                        mi[q] = ii;
+                    }
+                }
+            }
+        }
+        if (act) {
+            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
+#pragma unroll
+            for (int q = 0; q < CG; ++q) {
+                out[o + static_cast<size_t>(q) * PHW] = mv[q];
+                argmax[o + static_cast<size_t>(q) * PHW] = mi[q];
+            }
+        }
+    }
+}
+
 // nets/heads.py:42-47 (fp32 divide, then multiply) + [idx, box] pack.
 __global__ __launch_bounds__(256) void roi_transform_kernel(const float* __restrict__ rois,
                                                             const float* __restrict__ inds,
@@ -165,8 +376,9 @@ __global__ __launch_bounds__(256) void roi_bwd_prep_kernel(const float* __restri
 }
 
 // Ordered per-image RoI lists: list[b][*] = RoIs with batch index b, ascending.
+// Block N (the extra one) collects the RoIs whose batch index is outside [0, N).
 __global__ __launch_bounds__(1024) void roi_lists_kernel(const float* __restrict__ rois, int R,
-                                                         int* __restrict__ list,
+                                                         int N, int* __restrict__ list,
                                                          int* __restrict__ cnt) {
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -174,7 +386,8 @@ __global__ __launch_bounds__(1024) void roi_lists_kernel(const float* __restrict
     int base = 0;
     for (int r0 = 0; r0 < R; r0 += 1024) {
         int r = r0 + tid;
-        bool m = r < R && static_cast<int>(rois[static_cast<size_t>(r) * 5]) == b;
+        int rb = r < R ? static_cast<int>(rois[static_cast<size_t>(r) * 5]) : -1;
+        bool m = r < R && (b < N ? rb == b : (rb < 0 || rb >= N));
         uint64_t bal = __ballot(m);
         if (lane == 0) s_w[wid] = __popcll(bal);
         __syncthreads();
@@ -258,6 +471,22 @@ __global__ void roi_pool_bwd_kernel(const float* __restrict__ grad,
     }
 }
 
+// Outputs of RoIs with an out-of-range batch index: 0 / -1 (torchvision: UB).
+__global__ __launch_bounds__(256) void roi_pool_invalid_fill_kernel(const int* __restrict__ list,
+                                                                    const int* __restrict__ cnt,
+                                                                    int R, int N, size_t per_roi,
+                                                                    float* __restrict__ out,
+                                                                    int32_t* __restrict__ argmax) {
+    const int n = cnt[N];
+    for (int t = blockIdx.x; t < n; t += gridDim.x) {
+        const size_t base = static_cast<size_t>(list[static_cast<size_t>(N) * R + t]) * per_roi;
+        for (size_t e = threadIdx.x; e < per_roi; e += 256) {
+            out[base + e] = 0.0f;
+            argmax[base + e] = -1;
+        }
+    }
+}
+
 }  // namespace frcnn
 
 using namespace frcnn;
@@ -275,20 +504,85 @@ extern "C" int frcnn_roi_transform(const float* rois, const float* roi_inds, int
     return FRCNN_OK;
 }
 
+namespace {
+struct FwdWs {
+    int* list;
+    int* cnt;
+    size_t bytes;
+};
+FwdWs carve_fwd(void* ws, int64_t R, int N) {
+    Carver c(ws);
+    FwdWs w{};
+    w.list = c.take<int>(static_cast<size_t>(N + 1) * R);
+    w.cnt = c.take<int>(N + 1);
+    w.bytes = c.used();
+    return w;
+}
+constexpr int kFwdCG = 4;                       // channels per image tile
+constexpr size_t kFwdTileBudget = 96 * 1024;    // LDS for the CG planes
+}  // namespace
+
+extern "C" size_t frcnn_roi_pool_fwd_workspace_size(int64_t R, int N) {
+    if (R < 0 || N < 0) return 0;
+    return carve_fwd(nullptr, R, N).bytes;
+}
+
 extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, int N, int C,
                                   int H, int W, int PH, int PW, float spatial_scale, float* out,
-                                  int32_t* argmax, void* stream) {
+                                  int32_t* argmax, void* workspace, size_t ws_bytes,
+                                  void* stream) {
     FRCNN_REQUIRE(R >= 0 && N >= 0 && C >= 0 && H >= 0 && W >= 0, "frcnn_roi_pool_fwd: bad shape");
     FRCNN_REQUIRE(PH > 0 && PW > 0 && PH * PW <= kMaxBins,
                   "frcnn_roi_pool_fwd: output_size must have 1..%d bins", kMaxBins);
-    FRCNN_REQUIRE(R <= 0x7fffffff, "frcnn_roi_pool_fwd: too many rois");
+    FRCNN_REQUIRE(R <= 0x7fffffff && N <= 65535, "frcnn_roi_pool_fwd: too many rois / images");
     if (R == 0 || C == 0) return FRCNN_OK;
     FRCNN_REQUIRE(x && rois && out && argmax, "frcnn_roi_pool_fwd: null pointer");
-    const size_t total = static_cast<size_t>(C) * PH * PW;
-    const bool vec = (total % 4 == 0) && (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
-                     (reinterpret_cast<uintptr_t>(argmax) % 16 == 0);
     hipStream_t st = as_stream(stream);
-    if (vec)
+    const size_t HW = static_cast<size_t>(H) * W;
+    const size_t tile_bytes = kFwdCG * HW * sizeof(float);
+    const bool aligned = (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
+                         (reinterpret_cast<uintptr_t>(argmax) % 16 == 0);
+    if (N > 0 && C % kFwdCG == 0 && HW > 0 && tile_bytes <= kFwdTileBudget && aligned) {
+        FwdWs w = carve_fwd(workspace, R, N);
+        FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_fwd: workspace %zu < %zu",
+                      ws_bytes, w.bytes);
+        hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, rois,
+                           static_cast<int>(R), N, w.list, w.cnt);
+        FRCNN_LAUNCH_CHECK("roi_lists_kernel");
+        const int groups = C / kFwdCG;
+        const int64_t per_img = (R + N - 1) / N;
+        int64_t split = (1024 + static_cast<int64_t>(groups) * N - 1) / (static_cast<int64_t>(groups) * N);
+        int64_t cap = (per_img + 31) / 32;
+        split = split < cap ? split : cap;
+        split = split < 1 ? 1 : (split > 64 ? 64 : split);
+        const char* var = getenv("FRCNN_ROIPOOL_VARIANT");  // A/B override: tile | wave4 | wave8
+        const bool wave_ok = PH * PW <= 64;
+        if (wave_ok && !(var && var[0] == 't')) {
+            if (var && std::strcmp(var, "wave8") == 0 && C % 8 == 0 && 2 * tile_bytes <= kFwdTileBudget) {
+                dim3 grid(C / 8, N, static_cast<unsigned>(split));
+                hipLaunchKernelGGL(roi_pool_fwd_wave_kernel<8>, grid, dim3(kTileThreads), 2 * tile_bytes, st,
+                                   x, rois, w.list, w.cnt, static_cast<int>(R), C, H, W, PH, PW,
+                                   spatial_scale, out, argmax);
+            } else {
+                hipLaunchKernelGGL(roi_pool_fwd_wave_kernel<4>, dim3(groups, N, static_cast<unsigned>(split)),
+                                   dim3(kTileThreads), tile_bytes, st, x, rois, w.list, w.cnt,
+                                   static_cast<int>(R), C, H, W, PH, PW, spatial_scale, out, argmax);
+            }
+            FRCNN_LAUNCH_CHECK("roi_pool_fwd_wave_kernel");
+        } else {
+            hipLaunchKernelGGL(roi_pool_fwd_tile_kernel, dim3(groups, N, static_cast<unsigned>(split)),
+                               dim3(kTileThreads), tile_bytes, st, x, rois, w.list, w.cnt, static_cast<int>(R), C,
+                               H, W, PH, PW, kFwdCG, spatial_scale, out, argmax);
+            FRCNN_LAUNCH_CHECK("roi_pool_fwd_tile_kernel");
+        }
+        hipLaunchKernelGGL(roi_pool_invalid_fill_kernel, dim3(64), dim3(256), 0, st, w.list, w.cnt,
+                           static_cast<int>(R), N, static_cast<size_t>(C) * PH * PW, out, argmax);
+        FRCNN_LAUNCH_CHECK("roi_pool_invalid_fill_kernel");
+        return FRCNN_OK;
+    }
+    // generic path: one workgroup per RoI, gathers from L1/L2
+    const size_t total = static_cast<size_t>(C) * PH * PW;
+    if (total % 4 == 0 && aligned)
         hipLaunchKernelGGL(roi_pool_fwd_kernel<true>, dim3(static_cast<unsigned>(R)), dim3(256), 0,
                            st, x, rois, N, C, H, W, PH, PW, spatial_scale, out, argmax);
     else
@@ -309,8 +603,8 @@ BwdWs carve_bwd(void* ws, int64_t R, int N, int PH, int PW) {
     Carver c(ws);
     BwdWs w{};
     w.cmask = c.take<uint64_t>(static_cast<size_t>(R) * PH * PW);
-    w.list = c.take<int>(static_cast<size_t>(N) * R);
-    w.cnt = c.take<int>(N);
+    w.list = c.take<int>(static_cast<size_t>(N + 1) * R);
+    w.cnt = c.take<int>(N + 1);
     w.bytes = c.used();
     return w;
 }
@@ -346,8 +640,8 @@ extern "C" int frcnn_roi_pool_bwd(const float* grad, const float* rois, const in
     hipLaunchKernelGGL(roi_bwd_prep_kernel, dim3(static_cast<unsigned>(R)), dim3(256), 0, st, rois,
                        H, W, PH, PW, spatial_scale, w.cmask);
     FRCNN_LAUNCH_CHECK("roi_bwd_prep_kernel");
-    hipLaunchKernelGGL(roi_lists_kernel, dim3(N), dim3(1024), 0, st, rois, static_cast<int>(R),
-                       w.list, w.cnt);
+    hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, rois, static_cast<int>(R),
+                       N, w.list, w.cnt);
     FRCNN_LAUNCH_CHECK("roi_lists_kernel");
     const size_t plane_bytes = HW * sizeof(float);
     const int PHW = PH * PW;

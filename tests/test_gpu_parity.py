@@ -20,6 +20,13 @@ DEV = "cuda"
 RTOL = 1e-5
 
 
+@pytest.fixture(params=["fused", "wide"])
+def path(request, monkeypatch):
+    """Both proposal paths (fused per-image kernel / chip-wide bitmask NMS)."""
+    monkeypatch.setenv("FRCNN_PROPOSE_PATH", request.param)
+    return request.param
+
+
 def sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
@@ -58,7 +65,7 @@ def _propose_one_gpu(anchors, scores, deltas, img_w, img_h, pre, post):
 
 
 @pytest.mark.parametrize("case", [0, 1, 2])
-def test_propose_small_vs_reference(golden, case):
+def test_propose_small_vs_reference(golden, case, path):
     g = golden(f"proposal_small{case}.npz")
     anchors = orc.generate_anchors(orc.generate_anchor_base(), 16, int(g["feat_w"]), int(g["feat_h"]))
     rois, idx = _propose_one_gpu(anchors, g["scores"], g["deltas"], int(g["img_w"]), int(g["img_h"]),
@@ -73,7 +80,7 @@ def test_propose_small_vs_reference(golden, case):
 
 @pytest.mark.parametrize("cfg,imgs", [("cfg1", (0, 1)), ("cfg2", (0, 1, 2, 3)), ("cfg4", (0,)),
                                       ("cfg5", (0, 1))])
-def test_propose_batched_full_size(golden, cfg, imgs):
+def test_propose_batched_full_size(golden, cfg, imgs, path):
     """Batched path with in-kernel anchors at the BASELINE shapes."""
     g = golden("proposal_full.npz")
     c = synth.CONFIGS[cfg]
@@ -95,7 +102,7 @@ def test_propose_batched_full_size(golden, cfg, imgs):
         assert (idx[j, k:] == -1).all()
 
 
-def test_propose_batch_invariance():
+def test_propose_batch_invariance(path):
     """P-invariance: an image's proposals do not depend on its batch mates."""
     c = synth.CONFIGS["cfg2"]
     base = A.generate_anchor_base_device()
@@ -184,3 +191,50 @@ def test_roi_pool_bwd_deterministic():
     a = _roi_pool_bwd(g, rois, am, x.shape, 1.0)
     b = _roi_pool_bwd(g, rois, am, x.shape, 1.0)
     assert torch.equal(a, b)
+
+
+def test_roi_pool_out_of_range_batch_index():
+    """Extension: RoIs whose batch index is outside [0, N) pool to 0 / -1
+    (torchvision reads out of bounds there)."""
+    x = torch.randn(2, 8, 10, 12, device=DEV)
+    rois = torch.tensor([[-1, 0, 0, 5, 5], [1, 0, 0, 9, 9], [2, 1, 1, 4, 4], [7, 0, 0, 3, 3]],
+                        dtype=torch.float32, device=DEV)
+    out, am = ops.roi_pool_with_argmax(x, rois, 7)
+    assert (out[[0, 2, 3]] == 0).all() and (am[[0, 2, 3]] == -1).all()
+    oo, oa = orc.roi_pool_forward(x.cpu().numpy(), rois[1:2].cpu().numpy(), 7, 1.0)
+    assert np.array_equal(out[1:2].cpu().numpy(), oo) and np.array_equal(am[1:2].cpu().numpy(), oa)
+
+
+@pytest.mark.parametrize("case", ["ties", "pre1", "post_gt_kept", "all_filtered", "thr0", "thr1",
+                                  "chunk_edges"])
+def test_propose_edge_cases(case, path):
+    """Edge cases vs the oracle (ties ordered by ascending anchor index)."""
+    fh, fw, img_h, img_w = 20, 30, 320, 480
+    anchors = orc.generate_anchors(orc.generate_anchor_base(), 16, fw, fh)
+    n = len(anchors)
+    r = np.random.default_rng(hash(case) % 1000)
+    sc = synth.rpn_scores(n, 9, 0)
+    de = synth.rpn_deltas(n, 9, 0)
+    pre, post, thr = 3000, 300, 0.7
+    if case == "ties":
+        sc = (r.integers(0, 40, n) / 40).astype(np.float32)
+    elif case == "pre1":
+        pre, post = 1, 1
+    elif case == "post_gt_kept":
+        pre, post = 1025, 5000
+    elif case == "all_filtered":
+        de[:, 2:] = -6.0
+    elif case == "thr0":
+        thr = 0.0
+    elif case == "thr1":
+        thr, post = 1.0, 4000
+    elif case == "chunk_edges":
+        pre, post = 2049, 4000
+    rois, idx, cnt = ops.propose(torch.from_numpy(sc)[None].to(DEV), torch.from_numpy(de)[None].to(DEV),
+                                 img_w=img_w, img_h=img_h, pre_nms=pre, post_nms=post, nms_thresh=thr,
+                                 anchors=torch.from_numpy(anchors).to(DEV))
+    orois, oidx = orc.propose_one(anchors, sc, de, img_w, img_h, pre, post, nms_thresh=thr)
+    k = int(cnt[0])
+    assert k == len(oidx), (k, len(oidx))
+    assert np.array_equal(idx[0, :k].cpu().numpy(), oidx)
+    assert np.array_equal(rois[0, :k].cpu().numpy(), orois)

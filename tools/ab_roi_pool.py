@@ -1,0 +1,65 @@
+"""A/B timing of RoIPool forward variants on one device, interleaved rounds.
+
+    python tools/ab_roi_pool.py [--config cfg2] [--variants wave4,wave8,tile]
+
+Inputs are the bench's: cfg features + the proposals of the batch.  Every
+variant's output is checked bit-equal to the first variant's.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import make_inputs  # noqa: E402
+from replication_faster_rcnn_amd import anchors as A, ops, synth  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--variants", default="wave4,wave8,tile")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    c = synth.CONFIGS[a.config]
+    c, sc, de, x = make_inputs(a.config, c["batch"], 0, dev)
+    N = sc.size(0)
+    base = A.generate_anchor_base_device(anchor_scales=c["scales"])
+    rois, idx, cnt = ops.propose(sc, de, img_w=c["img_w"], img_h=c["img_h"], pre_nms=c["pre_nms"],
+                                 post_nms=c["post_nms"], anchor_base=base, feat_h=c["feat_h"],
+                                 feat_w=c["feat_w"])
+    inds = torch.arange(N, device=dev, dtype=torch.float32).repeat_interleave(c["post_nms"])
+    boxes = ops.roi_transform(rois.view(-1, 4), inds, c["img_h"], c["img_w"], c["feat_h"], c["feat_w"])
+    R = boxes.size(0)
+    C, H, W = x.shape[1:]
+    alg = N * C * H * W * 4 + R * 20 + 2 * R * C * 49 * 4
+    variants = a.variants.split(",")
+    ref = None
+    times = {v: [] for v in variants}
+    for rnd in range(a.rounds):
+        for v in variants:
+            os.environ["FRCNN_ROIPOOL_VARIANT"] = v
+            out, am = ops._roi_pool_fwd(x, boxes, 7, 7, 1.0)
+            if ref is None:
+                ref = (out.clone(), am.clone())
+            elif rnd == 0:
+                assert torch.equal(out, ref[0]) and torch.equal(am, ref[1]), f"variant {v} differs"
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                ops._roi_pool_fwd(x, boxes, 7, 7, 1.0)
+            e1.record()
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1) / a.iters * 1e3)
+    res = {v: {"us_median": float(np.median(t)), "us_min": float(np.min(t)),
+               "GBps": alg / (np.median(t) * 1e-6) / 1e9} for v, t in times.items()}
+    print(json.dumps({"config": a.config, "R": R, "alg_bytes": alg, "variants": res}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
