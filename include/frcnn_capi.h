@@ -105,7 +105,7 @@ int frcnn_roi_transform(const float* rois, const float* roi_inds, int64_t R, flo
  *   x fp32 [N,C,H,W], rois fp32 [R,5] -> out fp32 [R,C,PH,PW],
  *   argmax int32 [R,C,PH,PW] (h*W+w within the plane, -1 for empty bins).
  * RoIs whose batch index is outside [0,N) produce 0 / -1. */
-size_t frcnn_roi_pool_fwd_workspace_size(int64_t R, int N);
+size_t frcnn_roi_pool_fwd_workspace_size(int64_t R, int N, int C);
 int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
                        int PH, int PW, float spatial_scale, float* out, int32_t* argmax,
                        void* workspace, size_t ws_bytes, void* stream);

@@ -17,6 +17,7 @@
 // exactly the CPU order n -> ph -> pw.  The finished planes are stored once
 // (zero-fill of grad_in fused).
 #include <cfloat>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 
@@ -330,6 +331,294 @@ __global__ __launch_bounds__(kTileThreads) void roi_pool_fwd_wave_kernel(
     }
 }
 
+// Pixel-major variant: the LDS tile is [H*W][8] (8 channels of one pixel are
+// 32 contiguous bytes), so a lane reads its bin pixel for all 8 channels with
+// two ds_read_b128 from a single address -- no per-channel address math.
+template <int NT>
+__global__ __launch_bounds__(NT) void roi_pool_fwd_px8_kernel(
+    const float* __restrict__ x, const float* __restrict__ rois, const int* __restrict__ list,
+    const int* __restrict__ cnt, int* __restrict__ queue, int R, int C, int H, int W, int PH,
+    int PW, float ss, float* __restrict__ out, int32_t* __restrict__ argmax) {
+    constexpr int CG = 8;
+    extern __shared__ __attribute__((aligned(16))) float4 tile4[];  // [H*W][2] float4
+    const int b = blockIdx.y;
+    const int c0 = blockIdx.x * CG;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int HW = H * W;
+    const int PHW = PH * PW;
+    const int nr = cnt[b];
+    const int split = gridDim.z;
+    const int r_begin = static_cast<int>(static_cast<int64_t>(nr) * blockIdx.z / split);
+    const int r_end = static_cast<int>(static_cast<int64_t>(nr) * (blockIdx.z + 1) / split);
+    if (r_begin >= r_end) return;
+    // The waves pull this workgroup's RoIs from an LDS counter: RoI sizes vary
+    // a lot, a static round-robin leaves a long tail.
+    __shared__ int s_next;
+    if (tid == 0) s_next = r_begin;
+    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+    float* tile = reinterpret_cast<float*>(tile4);
+    for (int i = tid; i < CG * HW; i += NT) {
+        const int qq = i / HW, p = i - qq * HW;
+        tile[p * CG + qq] = src[i];
+    }
+    __syncthreads();
+    const int* lst = list + static_cast<size_t>(b) * R;
+    const int ph = lane / PW, pw = lane - (lane / PW) * PW;
+    const bool act = lane < PHW;
+    int t = 0;
+    if (lane == 0) t = atomicAdd(&s_next, 1);
+    t = __builtin_amdgcn_readfirstlane(t);
+    while (t < r_end) {
+        int tn = 0;
+        if (lane == 0) tn = atomicAdd(&s_next, 1);  // prefetch the next item
+        const int r = __builtin_amdgcn_readfirstlane(lst[t]);
+        const RoiGeom gm = roi_geom(rois + static_cast<size_t>(r) * 5, ss, PH, PW);
+        int4 g = geom_bin(gm, H, W, ph, pw);
+        if (!act) g = make_int4(0, 0, 0, 0);
+        const bool empty = g.y <= g.x || g.w <= g.z;
+        float mv[CG];
+        int mi[CG];
+#pragma unroll
+        for (int c = 0; c < CG; ++c) {
+            mv[c] = empty ? 0.0f : -FLT_MAX;
+            mi[c] = -1;
+        }
+        for (int h = g.x; h < g.y; ++h) {
+            int ii = h * W + g.z;
+            const int iend = h * W + g.w;
+            for (; ii < iend; ++ii) {
+                const float4 lo = tile4[2 * ii];
+                const float4 hi = tile4[2 * ii + 1];
+                const float v[CG] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+                for (int c = 0; c < CG; ++c) {
+                    if (v[c] > mv[c]) {
+                        mv[c] = v[c];
+                        mi[c] = ii;
+                    }
+                }
+            }
+        }
+        if (act) {
+            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
+#pragma unroll
+            for (int c = 0; c < CG; ++c) {
+                out[o + static_cast<size_t>(c) * PHW] = mv[c];
+                argmax[o + static_cast<size_t>(c) * PHW] = mi[c];
+            }
+        }
+        t = __builtin_amdgcn_readfirstlane(tn);
+    }
+}
+
+// Flattened, software-pipelined pixel-major variant.  The LDS tile is
+// [H*W+1][CG] (CG = 4 or 8 channels per pixel, one or two ds_read_b128); a lane
+// walks its bin window as ONE loop over bin_h*bin_w pixels (row-major, so the
+// strict-'>' first-max scan order is the reference's), loading pixel k+1
+// before comparing pixel k.  Waves pull RoIs from an LDS counter.
+template <int CG>
+__global__ __launch_bounds__(kTileThreads) void roi_pool_fwd_pxf_kernel(
+    const float* __restrict__ x, const float* __restrict__ rois, const int* __restrict__ list,
+    const int* __restrict__ cnt, int R, int C, int H, int W, int PH, int PW, float ss,
+    float* __restrict__ out, int32_t* __restrict__ argmax) {
+    constexpr int NV = CG / 4;  // float4 per pixel
+    extern __shared__ __attribute__((aligned(16))) float4 tile4[];  // [H*W + 1][NV]
+    __shared__ int s_next;
+    const int b = blockIdx.y;
+    const int c0 = blockIdx.x * CG;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int HW = H * W;
+    const int PHW = PH * PW;
+    const int nr = cnt[b];
+    const int split = gridDim.z;
+    const int r_begin = static_cast<int>(static_cast<int64_t>(nr) * blockIdx.z / split);
+    const int r_end = static_cast<int>(static_cast<int64_t>(nr) * (blockIdx.z + 1) / split);
+    if (r_begin >= r_end) return;
+    if (tid == 0) s_next = r_begin;
+    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+    float* tile = reinterpret_cast<float*>(tile4);
+    for (int i = tid; i < CG * HW; i += kTileThreads) {
+        const int qq = i / HW, p = i - qq * HW;
+        tile[p * CG + qq] = src[i];
+    }
+    if (tid < CG) tile[HW * CG + tid] = 0.0f;  // pad pixel: the prefetch may touch it
+    __syncthreads();
+    const int* lst = list + static_cast<size_t>(b) * R;
+    const int ph = lane / PW, pw = lane - (lane / PW) * PW;
+    const bool act = lane < PHW;
+    int t = 0;
+    if (lane == 0) t = atomicAdd(&s_next, 1);
+    t = __builtin_amdgcn_readfirstlane(t);
+    while (t < r_end) {
+        int tn = 0;
+        if (lane == 0) tn = atomicAdd(&s_next, 1);
+        const int r = __builtin_amdgcn_readfirstlane(lst[t]);
+        const RoiGeom gm = roi_geom(rois + static_cast<size_t>(r) * 5, ss, PH, PW);
+        int4 g = geom_bin(gm, H, W, ph, pw);
+        if (!act) g = make_int4(0, 0, 0, 0);
+        const int bwid = g.w - g.z;
+        const int bhgt = g.y - g.x;
+        const bool empty = bhgt <= 0 || bwid <= 0;
+        const int n = empty ? 0 : bhgt * bwid;
+        float mv[CG];
+        int mi[CG];
+#pragma unroll
+        for (int c = 0; c < CG; ++c) {
+            mv[c] = empty ? 0.0f : -FLT_MAX;
+            mi[c] = -1;
+        }
+        int ii = empty ? HW : g.x * W + g.z;  // HW = the pad pixel
+        const int jump = W - bwid + 1;
+        int col = 0;
+        float4 cur[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) cur[v] = tile4[ii * NV + v];
+        for (int k = 0; k < n; ++k) {
+            const int here = ii;
+            if (++col == bwid) {
+                col = 0;
+                ii += jump;
+            } else {
+                ++ii;
+            }
+            const int nx = ii < HW ? ii : HW;
+            float4 nxt[NV];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) nxt[v] = tile4[nx * NV + v];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const float vals[4] = {cur[v].x, cur[v].y, cur[v].z, cur[v].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (vals[e] > mv[4 * v + e]) {
+                        mv[4 * v + e] = vals[e];
+                        mi[4 * v + e] = here;
+                    }
+                }
+            }
+#pragma unroll
+            for (int v = 0; v < NV; ++v) cur[v] = nxt[v];
+        }
+        if (act) {
+            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
+#pragma unroll
+            for (int c = 0; c < CG; ++c) {
+                out[o + static_cast<size_t>(c) * PHW] = mv[c];
+                argmax[o + static_cast<size_t>(c) * PHW] = mi[c];
+            }
+        }
+        t = __builtin_amdgcn_readfirstlane(tn);
+    }
+}
+
+// Two-pass pixel-major variant (default).  The reference's strict-'>' scan
+// selects the FIRST element (row-major) equal to the window maximum among the
+// values > init (init = -FLT_MAX, or 0 for an empty bin).  So:
+//   pass 1: per bin row, rowmax = max3-chain over pixel pairs (0.5 VALU per
+//           channel-pixel); the running max keeps the FIRST row that raised it;
+//   pass 2: in that row only, the first pixel equal to the max gives the index
+//           and the output value (its exact bits, e.g. -0.0 vs +0.0).
+// NaN never wins in the reference; it is staged into LDS as -inf, which never
+// wins either.  A max not above init means "nothing selected": (init, -1).
+__device__ __forceinline__ float nan_to_ninf(float v) { return v != v ? -INFINITY : v; }
+
+__global__ __launch_bounds__(kTileThreads) void roi_pool_fwd_px8s_kernel(
+    const float* __restrict__ x, const float* __restrict__ rois, const int* __restrict__ list,
+    const int* __restrict__ cnt, int R, int C, int H, int W, int PH, int PW, float ss,
+    float* __restrict__ out, int32_t* __restrict__ argmax) {
+    constexpr int CG = 8;
+    extern __shared__ __attribute__((aligned(16))) float4 tile4[];  // [H*W][2] float4
+    const int b = blockIdx.y;
+    const int c0 = blockIdx.x * CG;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    constexpr int kWaves = kTileThreads / 64;
+    const int HW = H * W;
+    const int PHW = PH * PW;
+    const int nr = cnt[b];
+    const int split = gridDim.z;
+    const int r_begin = static_cast<int>(static_cast<int64_t>(nr) * blockIdx.z / split);
+    const int r_end = static_cast<int>(static_cast<int64_t>(nr) * (blockIdx.z + 1) / split);
+    if (r_begin >= r_end) return;
+    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+    float* tile = reinterpret_cast<float*>(tile4);
+    for (int i = tid; i < CG * HW; i += kTileThreads) {
+        const int q = i / HW, p = i - q * HW;
+        tile[p * CG + q] = nan_to_ninf(src[i]);
+    }
+    __syncthreads();
+    const int* lst = list + static_cast<size_t>(b) * R;
+    const int ph = lane / PW, pw = lane - (lane / PW) * PW;
+    const bool act = lane < PHW;
+    for (int t = r_begin + wid; t < r_end; t += kWaves) {
+        const int r = __builtin_amdgcn_readfirstlane(lst[t]);
+        const RoiGeom gm = roi_geom(rois + static_cast<size_t>(r) * 5, ss, PH, PW);
+        int4 g = geom_bin(gm, H, W, ph, pw);
+        if (!act) g = make_int4(0, 0, 0, 0);
+        const bool empty = g.y <= g.x || g.w <= g.z;
+        const float init = empty ? 0.0f : -FLT_MAX;
+        float mv[CG];
+        int brow[CG];
+#pragma unroll
+        for (int q = 0; q < CG; ++q) {
+            mv[q] = init;
+            brow[q] = -1;
+        }
+        const int wlast = g.w - 1;
+        for (int h = g.x; h < g.y; ++h) {
+            float rm[CG];
+#pragma unroll
+            for (int q = 0; q < CG; ++q) rm[q] = -INFINITY;
+            const int rb = h * W;
+            for (int w = g.z; w < g.w; w += 2) {
+                const int i0 = rb + w;
+                const int i1 = rb + min(w + 1, wlast);
+                const float4 a0 = tile4[2 * i0], a1 = tile4[2 * i0 + 1];
+                const float4 b0 = tile4[2 * i1], b1 = tile4[2 * i1 + 1];
+                rm[0] = fmaxf(fmaxf(rm[0], a0.x), b0.x);
+                rm[1] = fmaxf(fmaxf(rm[1], a0.y), b0.y);
+                rm[2] = fmaxf(fmaxf(rm[2], a0.z), b0.z);
+                rm[3] = fmaxf(fmaxf(rm[3], a0.w), b0.w);
+                rm[4] = fmaxf(fmaxf(rm[4], a1.x), b1.x);
+                rm[5] = fmaxf(fmaxf(rm[5], a1.y), b1.y);
+                rm[6] = fmaxf(fmaxf(rm[6], a1.z), b1.z);
+                rm[7] = fmaxf(fmaxf(rm[7], a1.w), b1.w);
+            }
+#pragma unroll
+            for (int q = 0; q < CG; ++q) {
+                if (rm[q] > mv[q]) {
+                    mv[q] = rm[q];
+                    brow[q] = h;
+                }
+            }
+        }
+        float ov[CG];
+        int oi[CG];
+#pragma unroll
+        for (int q = 0; q < CG; ++q) {
+            ov[q] = init;
+            oi[q] = -1;
+            if (brow[q] >= 0) {
+                const int rb = brow[q] * W;
+                for (int w = wlast; w >= g.z; --w) {  // reverse scan: last hit = first in order
+                    const float v = tile[(rb + w) * CG + q];
+                    if (v == mv[q]) {
+                        ov[q] = v;
+                        oi[q] = rb + w;
+                    }
+                }
+            }
+        }
+        if (act) {
+            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
+#pragma unroll
+            for (int q = 0; q < CG; ++q) {
+                out[o + static_cast<size_t>(q) * PHW] = ov[q];
+                argmax[o + static_cast<size_t>(q) * PHW] = oi[q];
+            }
+        }
+    }
+}
+
 // nets/heads.py:42-47 (fp32 divide, then multiply) + [idx, box] pack.
 __global__ __launch_bounds__(256) void roi_transform_kernel(const float* __restrict__ rois,
                                                             const float* __restrict__ inds,
@@ -377,9 +666,13 @@ __global__ __launch_bounds__(256) void roi_bwd_prep_kernel(const float* __restri
 
 // Ordered per-image RoI lists: list[b][*] = RoIs with batch index b, ascending.
 // Block N (the extra one) collects the RoIs whose batch index is outside [0, N).
+// Also zeroes the image's work-queue counters (`nq` per image) when given.
 __global__ __launch_bounds__(1024) void roi_lists_kernel(const float* __restrict__ rois, int R,
                                                          int N, int* __restrict__ list,
-                                                         int* __restrict__ cnt) {
+                                                         int* __restrict__ cnt,
+                                                         int* __restrict__ queue, int nq) {
+    if (queue && blockIdx.x < N)
+        for (int i = threadIdx.x; i < nq; i += 1024) queue[static_cast<size_t>(blockIdx.x) * nq + i] = 0;
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     __shared__ int s_w[16];
@@ -508,13 +801,15 @@ namespace {
 struct FwdWs {
     int* list;
     int* cnt;
+    int* queue;
     size_t bytes;
 };
-FwdWs carve_fwd(void* ws, int64_t R, int N) {
+FwdWs carve_fwd(void* ws, int64_t R, int N, int C) {
     Carver c(ws);
     FwdWs w{};
     w.list = c.take<int>(static_cast<size_t>(N + 1) * R);
     w.cnt = c.take<int>(N + 1);
+    w.queue = c.take<int>(static_cast<size_t>(N) * (C / 4 + 1));
     w.bytes = c.used();
     return w;
 }
@@ -522,9 +817,9 @@ constexpr int kFwdCG = 4;                       // channels per image tile
 constexpr size_t kFwdTileBudget = 96 * 1024;    // LDS for the CG planes
 }  // namespace
 
-extern "C" size_t frcnn_roi_pool_fwd_workspace_size(int64_t R, int N) {
-    if (R < 0 || N < 0) return 0;
-    return carve_fwd(nullptr, R, N).bytes;
+extern "C" size_t frcnn_roi_pool_fwd_workspace_size(int64_t R, int N, int C) {
+    if (R < 0 || N < 0 || C < 0) return 0;
+    return carve_fwd(nullptr, R, N, C).bytes;
 }
 
 extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, int N, int C,
@@ -543,11 +838,11 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
     const bool aligned = (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
                          (reinterpret_cast<uintptr_t>(argmax) % 16 == 0);
     if (N > 0 && C % kFwdCG == 0 && HW > 0 && tile_bytes <= kFwdTileBudget && aligned) {
-        FwdWs w = carve_fwd(workspace, R, N);
+        FwdWs w = carve_fwd(workspace, R, N, C);
         FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_fwd: workspace %zu < %zu",
                       ws_bytes, w.bytes);
         hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, rois,
-                           static_cast<int>(R), N, w.list, w.cnt);
+                           static_cast<int>(R), N, w.list, w.cnt, w.queue, C / 4);
         FRCNN_LAUNCH_CHECK("roi_lists_kernel");
         const int groups = C / kFwdCG;
         const int64_t per_img = (R + N - 1) / N;
@@ -555,10 +850,40 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
         int64_t cap = (per_img + 31) / 32;
         split = split < cap ? split : cap;
         split = split < 1 ? 1 : (split > 64 ? 64 : split);
+        // px8: 8-channel groups, >= 2 workgroups per CU, all sharing one queue per group
+        int64_t split8 = (512 + static_cast<int64_t>(C / 8) * N - 1) / (static_cast<int64_t>(C / 8) * N);
+        split8 = split8 < 1 ? 1 : (split8 > 64 ? 64 : split8);
         const char* var = getenv("FRCNN_ROIPOOL_VARIANT");  // A/B override: tile | wave4 | wave8
         const bool wave_ok = PH * PW <= 64;
         if (wave_ok && !(var && var[0] == 't')) {
-            if (var && std::strcmp(var, "wave8") == 0 && C % 8 == 0 && 2 * tile_bytes <= kFwdTileBudget) {
+            const size_t pad = 8 * sizeof(float);
+            if (var && std::strcmp(var, "pxf8") == 0 && C % 8 == 0 && 2 * tile_bytes + pad <= kFwdTileBudget) {
+                dim3 grid(C / 8, N, static_cast<unsigned>(split8));
+                hipLaunchKernelGGL(roi_pool_fwd_pxf_kernel<8>, grid, dim3(kTileThreads), 2 * tile_bytes + pad, st,
+                                   x, rois, w.list, w.cnt, static_cast<int>(R), C, H, W, PH, PW,
+                                   spatial_scale, out, argmax);
+            } else if (var && std::strcmp(var, "pxf4") == 0) {
+                dim3 grid(C / 4, N, static_cast<unsigned>(split));
+                hipLaunchKernelGGL(roi_pool_fwd_pxf_kernel<4>, grid, dim3(kTileThreads), tile_bytes + pad, st,
+                                   x, rois, w.list, w.cnt, static_cast<int>(R), C, H, W, PH, PW,
+                                   spatial_scale, out, argmax);
+            } else if (var && std::strcmp(var, "px8s") == 0 && C % 8 == 0 && 2 * tile_bytes <= kFwdTileBudget) {
+                dim3 grid(C / 8, N, static_cast<unsigned>(split));
+                hipLaunchKernelGGL(roi_pool_fwd_px8s_kernel, grid, dim3(kTileThreads), 2 * tile_bytes, st,
+                                   x, rois, w.list, w.cnt, static_cast<int>(R), C, H, W, PH, PW,
+                                   spatial_scale, out, argmax);
+            } else if (var && std::strcmp(var, "px8") == 0 && C % 8 == 0 && 2 * tile_bytes <= kFwdTileBudget) {
+                dim3 grid(C / 8, N, static_cast<unsigned>(split8));
+                hipLaunchKernelGGL(roi_pool_fwd_px8_kernel<512>, grid, dim3(512), 2 * tile_bytes, st,
+                                   x, rois, w.list, w.cnt, w.queue, static_cast<int>(R), C, H, W, PH, PW,
+                                   spatial_scale, out, argmax);
+            } else if (!(var && var[0] == 'w') && C % 8 == 0 && 2 * tile_bytes <= kFwdTileBudget) {
+                // default: 16-wave workgroups, two per CU share-nothing (2 x 77 KB LDS at 38x63)
+                dim3 grid(C / 8, N, static_cast<unsigned>(split8));
+                hipLaunchKernelGGL(roi_pool_fwd_px8_kernel<1024>, grid, dim3(1024), 2 * tile_bytes, st,
+                                   x, rois, w.list, w.cnt, w.queue, static_cast<int>(R), C, H, W, PH, PW,
+                                   spatial_scale, out, argmax);
+            } else if (var && std::strcmp(var, "wave8") == 0 && C % 8 == 0 && 2 * tile_bytes <= kFwdTileBudget) {
                 dim3 grid(C / 8, N, static_cast<unsigned>(split));
                 hipLaunchKernelGGL(roi_pool_fwd_wave_kernel<8>, grid, dim3(kTileThreads), 2 * tile_bytes, st,
                                    x, rois, w.list, w.cnt, static_cast<int>(R), C, H, W, PH, PW,
@@ -641,7 +966,7 @@ extern "C" int frcnn_roi_pool_bwd(const float* grad, const float* rois, const in
                        H, W, PH, PW, spatial_scale, w.cmask);
     FRCNN_LAUNCH_CHECK("roi_bwd_prep_kernel");
     hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, rois, static_cast<int>(R),
-                       N, w.list, w.cnt);
+                       N, w.list, w.cnt, nullptr, 0);
     FRCNN_LAUNCH_CHECK("roi_lists_kernel");
     const size_t plane_bytes = HW * sizeof(float);
     const int PHW = PH * PW;

@@ -1,0 +1,40 @@
+"""Second-stage head (nets/heads.py) on the HIP path.
+
+``ResnetHead.forward`` keeps the reference signature (nets/heads.py:27).  The
+RoI transform + ``[idx, box]`` pack (nets/heads.py:42-47) is one HIP kernel
+and RoIPool forward/backward (nets/heads.py:48) are the HIP kernels behind
+``ops.roi_pool``; the classifier (layer4 + avgpool) and the two FCs stay
+plain PyTorch (not the target).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import _lib, ops
+
+
+class ResnetHead(nn.Module):
+    def __init__(self, classifier, roi_size=7, spatial_scale=1, n_classes=21):
+        super().__init__()
+        self.classifier = classifier
+        self.reg = nn.Linear(in_features=512, out_features=n_classes * 4)
+        self.cls = nn.Linear(in_features=512, out_features=n_classes)
+        self.roi_size = roi_size
+        self.spatial_scale = spatial_scale
+
+    def forward(self, x, rois, roi_inds, img_h, img_w):
+        """-> (cls [N, n_classes, n_sample], reg [N, n_sample, n_classes*4])."""
+        N = x.shape[0]
+        dev = _lib.device()
+        r = torch.as_tensor(rois).detach().to(dev, torch.float32).contiguous()
+        ri = torch.as_tensor(roi_inds).detach().to(dev, torch.float32).contiguous()
+        boxes = ops.roi_transform(r, ri, img_h, img_w, x.shape[2], x.shape[3])
+        cropped = ops.roi_pool(x, boxes, (self.roi_size, self.roi_size), self.spatial_scale)
+        fc6 = self.classifier(cropped)
+        fc6 = fc6.view(fc6.shape[0], -1)
+        reg = self.reg(fc6)
+        cls = self.cls(fc6)
+        reg = reg.view(N, -1, reg.shape[-1])
+        cls = cls.view(N, -1, cls.shape[-1])
+        return cls.permute(0, 2, 1), reg

@@ -238,3 +238,47 @@ def test_propose_edge_cases(case, path):
     assert k == len(oidx), (k, len(oidx))
     assert np.array_equal(idx[0, :k].cpu().numpy(), oidx)
     assert np.array_equal(rois[0, :k].cpu().numpy(), orois)
+
+
+@pytest.mark.parametrize("variant", ["px8w16", "px8s", "px8", "pxf8", "pxf4", "wave8", "wave4", "tile"])
+def test_roi_pool_special_values(variant, monkeypatch):
+    """Signed zeros, -FLT_MAX, +-inf and NaN inside pooling windows: every
+    variant must reproduce the reference's strict-'>' first-max scan bit for bit."""
+    monkeypatch.setenv("FRCNN_ROIPOOL_VARIANT", variant)
+    r = np.random.default_rng(7)
+    N, C, H, W = 2, 16, 12, 14
+    x = r.standard_normal((N, C, H, W)).astype(np.float32)
+    x[0, 0] = 0.0
+    x[0, 0, ::2, ::3] = -0.0                       # +-0 ties: first zero's sign wins
+    x[0, 1] = -np.float32(3.4028235e38)            # all -FLT_MAX: nothing selected
+    x[0, 2] = -np.inf
+    x[0, 3, ::2] = np.nan
+    x[0, 4, 3:6, 3:6] = np.inf
+    x[1, 5] = np.nan
+    x[1, 6, :, 5] = 7.0                            # column plateau of equal maxima
+    x[1, 7] = -0.0
+    rois = np.array([[b, x1, y1, x1 + w, y1 + h] for b in range(N) for (x1, y1, w, h) in
+                     [(0, 0, 13, 11), (1, 2, 5, 3), (3, 3, 0, 0), (2, 1, 9, 9), (-3, -2, 20, 20)]],
+                    np.float32)
+    out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7)
+    oo, oa = orc.roi_pool_forward(x, rois, 7)
+    assert np.array_equal(am.cpu().numpy(), oa)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), oo.view(np.uint32))
+
+
+@pytest.mark.parametrize("variant", ["px8w16", "px8s", "px8", "pxf8", "pxf4", "wave8", "wave4", "tile"])
+def test_roi_pool_variants_random(variant, monkeypatch):
+    """Every forward variant, cfg2-like random RoIs, bit-exact vs the oracle."""
+    monkeypatch.setenv("FRCNN_ROIPOOL_VARIANT", variant)
+    r = np.random.default_rng(11)
+    N, C, H, W, R = 3, 32, 38, 63, 600
+    x = r.standard_normal((N, C, H, W), dtype=np.float32)
+    x[:, :, 10:20, 10:30] = np.round(x[:, :, 10:20, 10:30])  # plenty of ties
+    b = np.sort(r.integers(0, N, R)).astype(np.float32)
+    xy = r.uniform(-3, 60, (R, 2)).astype(np.float32)
+    wh = r.uniform(0, 40, (R, 2)).astype(np.float32)
+    rois = np.concatenate([b[:, None], xy, xy + wh], 1).astype(np.float32)
+    out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7)
+    oo, oa = orc.roi_pool_forward(x, rois, 7)
+    assert np.array_equal(am.cpu().numpy(), oa)
+    assert np.array_equal(out.cpu().numpy(), oo)
