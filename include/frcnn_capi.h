@@ -119,6 +119,52 @@ int frcnn_roi_pool_bwd(const float* grad, const float* rois, const int32_t* argm
                        int N, int C, int H, int W, int PH, int PW, float spatial_scale,
                        float* grad_in, void* workspace, size_t ws_bytes, void* stream);
 
+
+/* --------------------------------------------------------- target creators */
+
+/* utils/utils.py:102 bbox_iou(bbox_a, bbox_b) -> [na, nb], with numpy's dtype
+ * promotion: a, b each fp32 or fp64 (flag); out fp32 if both fp32, else fp64. */
+int frcnn_bbox_iou(const void* a, int a_is_f64, int64_t na, const void* b, int b_is_f64,
+                   int64_t nb, void* out, void* stream);
+
+/* utils/utils.py:75 bbox2reg(anchors, bbox) -> fp64 [n, 4] (anchor statistics in
+ * the anchors' dtype, box statistics in the boxes' dtype, as numpy does). */
+int frcnn_bbox2reg(const void* anchors, int a_is_f64, const void* bbox, int b_is_f64, int64_t n,
+                   double* out, void* stream);
+
+/* utils/utils.py:122-204 AnchorTargetCreator.__call__, batched over N images in
+ * the order of train.py:71-79.
+ *   anchors fp32 [A,4]; boxes fp64 [N,G,4] + labels fp64 [N,G] (rows with label
+ *   -1 are padding, train.py:74-76; G <= 256)
+ *   rng_state u32 [625] = numpy legacy MT19937 key[624] + pos, updated in place
+ *   exactly as the reference's np.random.choice calls would; NULL = no sampling
+ *   (labels before the disable step, no RNG use)
+ * Outputs: reg fp64 [N,A,4] (zeros for an image without gt), label int32 [N,A],
+ * optional argmax int32 [N,A] (after the gt override, utils/utils.py:171-172) and
+ * max_iou fp64 [N,A]. */
+size_t frcnn_anchor_target_workspace_size(int N, int A, int G);
+int frcnn_anchor_target(int N, int A, int G, const float* anchors, const double* boxes,
+                        const double* labels, int n_sample, double pos_iou_thresh,
+                        double neg_iou_thresh, double pos_ratio, uint32_t* rng_state,
+                        double* reg, int32_t* label, int32_t* argmax, double* max_iou,
+                        void* workspace, size_t ws_bytes, void* stream);
+
+/* utils/utils.py:207-276 ProposalTargetCreator.__call__, batched over N images in
+ * the order of train.py:91-104.
+ *   rois fp32 [N,Rp,4] with rcount int32 [N] valid rows per image; boxes/labels as
+ *   for frcnn_anchor_target; reg_mean / reg_std: HOST fp64 [4] (the fp32 values of
+ *   utils/utils.py:272 widened); rng_state as above (required).
+ * Outputs (padded to n_sample): sample_roi fp64 [N,n_sample,4], gt_roi_reg fp64
+ * [N,n_sample,4], gt_roi_label fp64 [N,n_sample], sample_count int32 [N]. */
+size_t frcnn_proposal_target_workspace_size(int N, int Rp, int G, int n_sample);
+int frcnn_proposal_target(int N, int Rp, const float* rois, const int32_t* rcount, int G,
+                          const double* boxes, const double* labels, int n_sample,
+                          double pos_ratio, double pos_iou_thresh, double neg_iou_thresh_high,
+                          double neg_iou_thresh_low, const double* reg_mean,
+                          const double* reg_std, uint32_t* rng_state, double* sample_roi,
+                          double* gt_roi_reg, double* gt_roi_label, int32_t* sample_count,
+                          void* workspace, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -51,6 +51,14 @@ SIGNATURES = {
     "frcnn_roi_pool_fwd": (I32, [P, P, I64, I32, I32, I32, I32, I32, I32, F32, P, P, P, SZ, P]),
     "frcnn_roi_pool_bwd_workspace_size": (SZ, [I64, I32, I32, I32]),
     "frcnn_roi_pool_bwd": (I32, [P, P, P, I64, I32, I32, I32, I32, I32, I32, F32, P, P, SZ, P]),
+    "frcnn_bbox_iou": (I32, [P, I32, I64, P, I32, I64, P, P]),
+    "frcnn_bbox2reg": (I32, [P, I32, P, I32, I64, P, P]),
+    "frcnn_anchor_target_workspace_size": (SZ, [I32, I32, I32]),
+    "frcnn_anchor_target": (I32, [I32, I32, I32, P, P, P, I32, F64, F64, F64, P, P, P, P, P, P,
+                                  SZ, P]),
+    "frcnn_proposal_target_workspace_size": (SZ, [I32, I32, I32, I32]),
+    "frcnn_proposal_target": (I32, [I32, I32, P, P, I32, P, P, I32, F64, F64, F64, F64, P, P, P,
+                                    P, P, P, P, P, SZ, P]),
 }
 
 _lib = None

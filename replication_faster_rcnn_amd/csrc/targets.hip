@@ -1,0 +1,897 @@
+// Target assignment (utils/utils.py:102-276) on gfx950: fp64 IoU matching,
+// anchor/proposal labels and numpy-RNG-exact sampling.
+//
+// IoU: numpy's dtype promotion and op order of utils/utils.py:114-119, in fp64
+// (anchors fp32, gt fp64 -> fp64; both fp32 -> fp32).  argmax = first maximum,
+// NaN first (numpy rules).
+//
+// Sampling: the reference calls np.random.choice(arr, k, replace=False) on the
+// GLOBAL legacy RandomState (utils/utils.py:194,201,251,258), which is
+// arr[permutation(len(arr))[:k]]; permutation is Fisher-Yates
+//   for i = n-1 .. 1: j = random_interval(i); swap(a[i], a[j])
+// with random_interval = "next MT19937 word & mask(i), reject while > i".
+// The caller hands the MT19937 state (624 words + pos) in and gets it back,
+// so the numpy global stream continues exactly as after the reference's calls.
+//  * one wave runs the rejection automaton 64 words at a time: lane l owns
+//    word l; which words are accepted depends on how many earlier lanes
+//    accepted, solved as a fixed point over ballots (<= 64 rounds, ~2-3);
+//  * the twist is done by the same wave, 64 state words per step (the
+//    recurrence reaches back 227 / forward 397 words, both > 64);
+//  * only the permutation positions the caller needs are reconstructed, by
+//    tracing each position backwards through the recorded swaps (lanes in
+//    parallel): the last m positions for AnchorTarget (which m elements
+//    survive the disable), the first k for ProposalTarget (in order).
+#include <cfloat>
+#include <cmath>
+
+#include "common.h"
+
+namespace frcnn {
+
+// ------------------------------------------------------------------ IoU core
+// numpy: tl = max(a[:2], b[:2]); br = min(a[2:], b[2:]);
+//        inter = prod(br - tl) * all(tl < br); area_a = prod(a[2:] - a[:2]) (a's dtype)
+//        iou = inter / (area_a + area_b - inter)
+// np.maximum / np.minimum: NaN propagates.
+template <class T>
+__device__ __forceinline__ T np_max(T a, T b) { return (a != a || a >= b) ? a : b; }
+template <class T>
+__device__ __forceinline__ T np_min(T a, T b) { return (a != a || a <= b) ? a : b; }
+
+template <class TA>
+__device__ __forceinline__ double iou_np(const TA* a, double area_a_as_f64, const double* b,
+                                         double area_b) {
+    double tl0 = np_max(static_cast<double>(a[0]), b[0]);
+    double tl1 = np_max(static_cast<double>(a[1]), b[1]);
+    double br0 = np_min(static_cast<double>(a[2]), b[2]);
+    double br1 = np_min(static_cast<double>(a[3]), b[3]);
+    double inter = (br0 - tl0) * (br1 - tl1);
+    inter = inter * ((tl0 < br0 && tl1 < br1) ? 1.0 : 0.0);
+    double uni = area_a_as_f64 + area_b;
+    uni = uni - inter;
+    return inter / uni;
+}
+
+template <class T>
+__device__ __forceinline__ T area_np(const T* a) {
+    T d0 = a[2] - a[0];
+    T d1 = a[3] - a[1];
+    return d0 * d1;
+}
+
+// numpy max/argmax "better" relation: NaN wins (first NaN), else larger, ties -> earlier.
+__device__ __forceinline__ bool np_better(double v, double cur, bool cur_nan) {
+    if (cur_nan) return false;
+    if (v != v) return true;
+    return v > cur;
+}
+
+// ------------------------------------------------------------ gt compaction
+// Rows with label == -1 are padding (utils/data_loader.py:88-89, train.py:74-76).
+__global__ __launch_bounds__(64) void gt_compact_kernel(const double* __restrict__ boxes,
+                                                        const double* __restrict__ labels,
+                                                        int Gp, double* __restrict__ gt,
+                                                        double* __restrict__ gl,
+                                                        int* __restrict__ gcount) {
+    const int n = blockIdx.x, lane = threadIdx.x;
+    int base = 0;
+    for (int g0 = 0; g0 < Gp; g0 += 64) {
+        const int g = g0 + lane;
+        const bool v = g < Gp && labels[static_cast<size_t>(n) * Gp + g] != -1.0;
+        const uint64_t bal = __ballot(v);
+        if (v) {
+            const int o = base + __popcll(bal & lanemask_lt());
+            for (int c = 0; c < 4; ++c)
+                gt[(static_cast<size_t>(n) * Gp + o) * 4 + c] = boxes[(static_cast<size_t>(n) * Gp + g) * 4 + c];
+            gl[static_cast<size_t>(n) * Gp + o] = labels[static_cast<size_t>(n) * Gp + g];
+        }
+        base += __popcll(bal);
+    }
+    if (lane == 0) gcount[n] = base;
+}
+
+// --------------------------------------------------------- AnchorTarget IoU
+constexpr int kMaxG = 256;
+
+struct ArgMax {
+    double v;
+    int i;
+    int nan;
+};
+
+__device__ __forceinline__ ArgMax am_combine(ArgMax a, ArgMax b) {  // a precedes b
+    if (a.nan) return a;
+    if (b.nan) return b;
+    if (b.v > a.v) return b;
+    return a;
+}
+
+// grid (ceil(A/256), N): per anchor row max/argmax over the image's gt, and per
+// block the column (max, first anchor) partial of every gt.
+__global__ __launch_bounds__(256) void at_iou_kernel(const float* __restrict__ anchors, int A,
+                                                     const double* __restrict__ gt,
+                                                     const int* __restrict__ gcount, int Gp,
+                                                     int32_t* __restrict__ row_arg,
+                                                     double* __restrict__ row_max,
+                                                     double* __restrict__ col_v,
+                                                     int* __restrict__ col_i) {
+    __shared__ double sg[kMaxG][4];
+    __shared__ double sa[kMaxG];
+    __shared__ ArgMax wred[4][kMaxG];
+    const int n = blockIdx.y;
+    const int G = gcount[n];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int g = tid; g < G; g += 256) {
+        for (int c = 0; c < 4; ++c) sg[g][c] = gt[(static_cast<size_t>(n) * Gp + g) * 4 + c];
+        sa[g] = area_np(sg[g]);
+    }
+    __syncthreads();
+    const int a = blockIdx.x * 256 + tid;
+    const bool va = a < A;
+    float box[4] = {0.f, 0.f, 0.f, 0.f};
+    if (va)
+        for (int c = 0; c < 4; ++c) box[c] = anchors[static_cast<size_t>(a) * 4 + c];
+    const double aa = static_cast<double>(area_np(box));  // fp32 product, then promoted
+    ArgMax best{0.0, 0, 0};
+    for (int g = 0; g < G; ++g) {
+        const double v = iou_np(box, aa, sg[g], sa[g]);
+        if (g == 0) {
+            best.v = v;
+            best.i = 0;
+            best.nan = v != v;
+        } else if (np_better(v, best.v, best.nan)) {
+            best.v = v;
+            best.i = g;
+            best.nan = v != v;
+        }
+        // column partial: first anchor of this block with the best value
+        ArgMax c{va ? v : -INFINITY, va ? a : 0x7fffffff, (va && v != v) ? 1 : 0};
+        for (int o = 1; o < 64; o <<= 1) {  // ordered reduction over lanes
+            ArgMax other;
+            other.v = __shfl_down(c.v, o, 64);
+            other.i = __shfl_down(c.i, o, 64);
+            other.nan = __shfl_down(c.nan, o, 64);
+            if ((lane & (2 * o - 1)) == 0 && lane + o < 64) c = am_combine(c, other);
+        }
+        if (lane == 0) wred[wid][g] = c;
+    }
+    if (va) {
+        row_arg[static_cast<size_t>(n) * A + a] = G > 0 ? best.i : 0;
+        row_max[static_cast<size_t>(n) * A + a] = G > 0 ? best.v : 0.0;
+    }
+    __syncthreads();
+    for (int g = tid; g < G; g += 256) {
+        ArgMax c = wred[0][g];
+        for (int w = 1; w < 4; ++w) c = am_combine(c, wred[w][g]);
+        const size_t o = (static_cast<size_t>(n) * gridDim.x + blockIdx.x) * Gp + g;
+        col_v[o] = c.nan ? NAN : c.v;
+        col_i[o] = c.i;
+    }
+}
+
+// grid N, 1024 threads: gt_argmax from the block partials, labels of
+// utils/utils.py:176-188 and the ordered pos / neg index lists.
+__global__ __launch_bounds__(1024) void at_label_kernel(
+    int A, int Gp, int nblk, const int* __restrict__ gcount, const double* __restrict__ row_max,
+    const double* __restrict__ col_v, const int* __restrict__ col_i, double neg_thr, double pos_thr,
+    int32_t* __restrict__ row_arg, int8_t* __restrict__ label0, int* __restrict__ pos_list,
+    int* __restrict__ neg_list, int* __restrict__ npos, int* __restrict__ nneg) {
+    __shared__ int s_garg[kMaxG];
+    __shared__ int s_w[16];
+    const int n = blockIdx.x;
+    const int G = gcount[n];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int g = tid; g < G; g += 1024) {
+        ArgMax c{0.0, 0, 0};
+        for (int b = 0; b < nblk; ++b) {
+            const size_t o = (static_cast<size_t>(n) * nblk + b) * Gp + g;
+            const double v = col_v[o];
+            ArgMax x{v, col_i[o], v != v};
+            c = b == 0 ? x : am_combine(c, x);
+        }
+        s_garg[g] = c.i;
+    }
+    __syncthreads();
+    int8_t* lab = label0 + static_cast<size_t>(n) * A;
+    const double* mx = row_max + static_cast<size_t>(n) * A;
+    for (int a = tid; a < A; a += 1024) {
+        int8_t l = -1;
+        const double m = mx[a];
+        if (m < neg_thr) l = 0;
+        if (m >= pos_thr) l = 1;
+        lab[a] = l;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int32_t* arg = row_arg + static_cast<size_t>(n) * A;
+        for (int g = 0; g < G; ++g) {      // utils/utils.py:171-172 (later gt wins) and :187-188
+            arg[s_garg[g]] = g;
+            lab[s_garg[g]] = 1;
+        }
+    }
+    __syncthreads();
+    // ordered compaction of label==1 and label==0 positions
+    int pbase = 0, nbase = 0;
+    for (int a0 = 0; a0 < A; a0 += 1024) {
+        const int a = a0 + tid;
+        const int8_t l = a < A ? lab[a] : -1;
+        const uint64_t bp = __ballot(l == 1), bn = __ballot(l == 0);
+        const int cp = __popcll(bp), cn = __popcll(bn);
+        if (lane == 0) s_w[wid] = cp | (cn << 16);
+        __syncthreads();
+        int bpp = 0, bnn = 0, tp = 0, tn = 0;
+        for (int w = 0; w < 16; ++w) {
+            const int v = s_w[w];
+            if (w < wid) {
+                bpp += v & 0xffff;
+                bnn += v >> 16;
+            }
+            tp += v & 0xffff;
+            tn += v >> 16;
+        }
+        if (l == 1) pos_list[static_cast<size_t>(n) * A + pbase + bpp + __popcll(bp & lanemask_lt())] = a;
+        if (l == 0) neg_list[static_cast<size_t>(n) * A + nbase + bnn + __popcll(bn & lanemask_lt())] = a;
+        pbase += tp;
+        nbase += tn;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        npos[n] = pbase;
+        nneg[n] = nbase;
+    }
+}
+
+// ------------------------------------------------------------- MT19937 wave
+constexpr int kMtN = 624;
+constexpr int kMtM = 397;
+
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+// One wave regenerates the 624-word state in place (numpy mt19937_gen).
+__device__ void mt_twist_wave(uint32_t* key) {
+    const int lane = lane_id();
+    for (int c = 0; c < 10; ++c) {
+        const int i = c * 64 + lane;
+        uint32_t nv = 0;
+        if (i < kMtN - 1) {
+            const uint32_t y = (key[i] & 0x80000000u) | (key[i + 1] & 0x7fffffffu);
+            const uint32_t src = i < kMtN - kMtM ? key[i + kMtM] : key[i - (kMtN - kMtM)];
+            nv = src ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (i < kMtN - 1) key[i] = nv;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (lane == 0) {
+        const uint32_t y = (key[kMtN - 1] & 0x80000000u) | (key[0] & 0x7fffffffu);
+        key[kMtN - 1] = key[kMtM - 1] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+__device__ __forceinline__ uint32_t mask_for(uint32_t v) {
+    v |= v >> 1;
+    v |= v >> 2;
+    v |= v >> 4;
+    v |= v >> 8;
+    v |= v >> 16;
+    return v;
+}
+
+// Run Fisher-Yates steps i = i_hi .. i_lo (descending) on the stream; for
+// steps with i >= rec_lo store J[i - rec_lo] = j.  Wave-uniform; `pos` is the
+// stream position (shared scalar), state in `key`.
+__device__ void fy_steps_wave(uint32_t* key, int& pos, int i_hi, int i_lo, int rec_lo, int* J) {
+    const int lane = lane_id();
+    int i_cur = i_hi;
+    while (i_cur >= i_lo) {
+        if (pos == kMtN) {
+            mt_twist_wave(key);
+            pos = 0;
+        }
+        const int cnt = min(64, kMtN - pos);
+        const uint32_t w = lane < cnt ? mt_temper(key[pos + lane]) : 0u;
+        uint64_t acc = cnt == 64 ? ~0ull : ((1ull << cnt) - 1ull);
+        int il = 0;
+        uint32_t m = 0;
+        bool a = false;
+        for (int it = 0; it < 65; ++it) {
+            il = i_cur - __popcll(acc & lanemask_lt());
+            const bool valid = lane < cnt && il >= i_lo;
+            m = valid ? mask_for(static_cast<uint32_t>(il)) : 0u;
+            a = valid && (w & m) <= static_cast<uint32_t>(il);
+            const uint64_t acc2 = __ballot(a);
+            if (acc2 == acc) break;
+            acc = acc2;
+        }
+        if (a && il >= rec_lo) J[il - rec_lo] = static_cast<int>(w & m);
+        const int na = __popcll(acc);
+        int consumed = cnt;
+        if (i_cur - na < i_lo) consumed = 64 - __clzll(acc);  // last accepted lane + 1
+        i_cur -= na;
+        pos += consumed;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// Final value at permutation position p (identity start), given J[i - rec_lo]
+// for every step i >= rec_lo of the n-element shuffle.  Requires p >= rec_lo.
+__device__ __forceinline__ int fy_trace(int p, int n, int rec_lo, const int* J) {
+    int cur = p;
+    for (int i = (p > 1 ? p : 1); i < n; ++i) {
+        const int j = J[i - rec_lo];
+        if (cur == i) cur = j;
+        else if (cur == j) cur = i;
+    }
+    return cur;
+}
+
+// ---------------------------------------------------------- AnchorTarget RNG
+// One workgroup: for each image in order, the two choice() calls of
+// utils/utils.py:190-202.  Kept anchors are marked in keep[n][a] (zeroed by
+// the caller); pos_sampled / neg_sampled record whether a call happened.
+constexpr int kMaxKeep = 4096;
+
+__global__ __launch_bounds__(256) void at_sample_kernel(
+    int N, int A, int n_sample, int n_pos_max, const int* __restrict__ pos_list,
+    const int* __restrict__ neg_list, const int* __restrict__ npos, const int* __restrict__ nneg,
+    uint32_t* __restrict__ rng, uint8_t* __restrict__ keep, int* __restrict__ sampled) {
+    __shared__ uint32_t key[kMtN];
+    __shared__ int J[kMaxKeep];
+    __shared__ int s_pos;
+    const int tid = threadIdx.x, wid = tid >> 6;
+    for (int i = tid; i < kMtN; i += 256) key[i] = rng[i];
+    if (tid == 0) s_pos = static_cast<int>(rng[kMtN]);
+    __syncthreads();
+    for (int n = 0; n < N; ++n) {
+        const int P = npos[n];
+        const int Q = nneg[n];
+        const int pos_after = P > n_pos_max ? n_pos_max : P;
+        const int neg_keep = n_sample - pos_after;
+        for (int call = 0; call < 2; ++call) {
+            const int cnt = call == 0 ? P : Q;
+            const int m = call == 0 ? n_pos_max : neg_keep;  // survivors
+            const bool do_call = cnt > m;
+            if (tid == 0) sampled[2 * n + call] = do_call ? 1 : 0;
+            if (!do_call) continue;
+            const int k = cnt - m;  // disabled = perm[:k]; survivors = perm[k:]
+            if (wid == 0) {
+                int pos = s_pos;
+                fy_steps_wave(key, pos, cnt - 1, 1, k, J);
+                if (lane_id() == 0) s_pos = pos;
+            }
+            __syncthreads();
+            const int* lst = (call == 0 ? pos_list : neg_list) + static_cast<size_t>(n) * A;
+            for (int p = k + tid; p < cnt; p += 256) {  // survivors, any order
+                const int v = fy_trace(p, cnt, k, J);  // p >= k >= 1
+                keep[static_cast<size_t>(n) * A + lst[v]] = 1;
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = tid; i < kMtN; i += 256) rng[i] = key[i];
+    if (tid == 0) rng[kMtN] = static_cast<uint32_t>(s_pos);
+}
+
+// grid (ceil(A/256), N): final label (after disabling) and regression target
+// bbox2reg(anchor, bbox[argmax]) (utils/utils.py:75-100,146-150; anchor stats
+// fp32, box stats fp64).
+__global__ __launch_bounds__(256) void at_finish_kernel(
+    const float* __restrict__ anchors, int A, const double* __restrict__ gt,
+    const int* __restrict__ gcount, int Gp, const int32_t* __restrict__ row_arg,
+    const int8_t* __restrict__ label0, const uint8_t* __restrict__ keep,
+    const int* __restrict__ sampled, int32_t* __restrict__ label, double* __restrict__ reg) {
+    const int n = blockIdx.y;
+    const int a = blockIdx.x * 256 + threadIdx.x;
+    if (a >= A) return;
+    const size_t o = static_cast<size_t>(n) * A + a;
+    const int8_t l0 = label0[o];
+    int32_t l = -1;
+    if (l0 == 1) l = (!sampled[2 * n] || keep[o]) ? 1 : -1;
+    else if (l0 == 0) l = (!sampled[2 * n + 1] || keep[o]) ? 0 : -1;
+    label[o] = l;
+    const int G = gcount[n];
+    double* r = reg + o * 4;
+    if (G == 0) {
+        r[0] = r[1] = r[2] = r[3] = 0.0;
+        return;
+    }
+    const float* an = anchors + static_cast<size_t>(a) * 4;
+    const double* b = gt + (static_cast<size_t>(n) * Gp + row_arg[o]) * 4;
+    const float ah = an[2] - an[0];
+    const float aw = an[3] - an[1];
+    const float acx = (an[2] + an[0]) / 2.0f;
+    const float acy = (an[1] + an[3]) / 2.0f;
+    const double bh = b[2] - b[0];
+    const double bw = b[3] - b[1];
+    const double bcx = (b[2] + b[0]) / 2.0;
+    const double bcy = (b[1] + b[3]) / 2.0;
+    r[0] = (bcx - static_cast<double>(acx)) / static_cast<double>(ah);
+    r[1] = (bcy - static_cast<double>(acy)) / static_cast<double>(aw);
+    r[2] = log(bh / static_cast<double>(ah));
+    r[3] = log(bw / static_cast<double>(aw));
+}
+
+// ----------------------------------------------------- ProposalTarget (f64)
+// grid N, 1024 threads: roi_all = concat(roi fp32 -> fp64, gt), IoU with the gt,
+// row argmax / max, label of the assigned gt, ordered pos / neg lists
+// (utils/utils.py:229-258).
+__global__ __launch_bounds__(1024) void pt_iou_kernel(
+    const float* __restrict__ rois, const int* __restrict__ rcount, int Rp,
+    const double* __restrict__ gt, const double* __restrict__ gl, const int* __restrict__ gcount,
+    int Gp, double pos_thr, double neg_hi, double neg_lo, double* __restrict__ roi_all,
+    int32_t* __restrict__ assign, int* __restrict__ pos_list, int* __restrict__ neg_list,
+    int* __restrict__ npos, int* __restrict__ nneg) {
+    __shared__ double sg[kMaxG][4];
+    __shared__ double sa[kMaxG];
+    __shared__ int s_w[16];
+    const int n = blockIdx.x;
+    const int G = gcount[n];
+    const int Rn = rcount[n];
+    const int T = Rn + G;
+    const int stride = Rp + Gp;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int g = tid; g < G; g += 1024) {
+        for (int c = 0; c < 4; ++c) sg[g][c] = gt[(static_cast<size_t>(n) * Gp + g) * 4 + c];
+        sa[g] = area_np(sg[g]);
+    }
+    __syncthreads();
+    int pbase = 0, nbase = 0;
+    for (int t0 = 0; t0 < T; t0 += 1024) {
+        const int t = t0 + tid;
+        bool isp = false, isn = false;
+        if (t < T) {
+            double box[4];
+            for (int c = 0; c < 4; ++c)
+                box[c] = t < Rn ? static_cast<double>(rois[(static_cast<size_t>(n) * Rp + t) * 4 + c])
+                                : sg[t - Rn][c];
+            for (int c = 0; c < 4; ++c) roi_all[(static_cast<size_t>(n) * stride + t) * 4 + c] = box[c];
+            const double ab = area_np(box);
+            double best = 0.0;
+            int bi = 0;
+            bool bnan = false;
+            for (int g = 0; g < G; ++g) {
+                const double v = iou_np(box, ab, sg[g], sa[g]);
+                if (g == 0) {
+                    best = v;
+                    bnan = v != v;
+                } else if (np_better(v, best, bnan)) {
+                    best = v;
+                    bi = g;
+                    bnan = v != v;
+                }
+            }
+            if (G == 0) best = 0.0;
+            assign[static_cast<size_t>(n) * stride + t] = bi;
+            isp = best >= pos_thr;
+            isn = best < neg_hi && best >= neg_lo;
+        }
+        const uint64_t bp = __ballot(isp), bn = __ballot(isn);
+        if (lane == 0) s_w[wid] = __popcll(bp) | (__popcll(bn) << 16);
+        __syncthreads();
+        int bpp = 0, bnn = 0, tp = 0, tn = 0;
+        for (int w = 0; w < 16; ++w) {
+            const int v = s_w[w];
+            if (w < wid) {
+                bpp += v & 0xffff;
+                bnn += v >> 16;
+            }
+            tp += v & 0xffff;
+            tn += v >> 16;
+        }
+        if (isp) pos_list[static_cast<size_t>(n) * stride + pbase + bpp + __popcll(bp & lanemask_lt())] = t;
+        if (isn) neg_list[static_cast<size_t>(n) * stride + nbase + bnn + __popcll(bn & lanemask_lt())] = t;
+        pbase += tp;
+        nbase += tn;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        npos[n] = pbase;
+        nneg[n] = nbase;
+    }
+}
+
+// One workgroup: the two choice() calls of utils/utils.py:248-258 per image,
+// in image order; sample order = pos perm prefix, then neg perm prefix.
+__global__ __launch_bounds__(256) void pt_sample_kernel(
+    int N, int stride, int n_sample, int pos_per_image, const int* __restrict__ pos_list,
+    const int* __restrict__ neg_list, const int* __restrict__ npos, const int* __restrict__ nneg,
+    uint32_t* __restrict__ rng, int* __restrict__ sample, int* __restrict__ scount,
+    int* __restrict__ spos) {
+    __shared__ uint32_t key[kMtN];
+    __shared__ int J[kMaxKeep];
+    __shared__ int s_pos;
+    const int tid = threadIdx.x, wid = tid >> 6;
+    for (int i = tid; i < kMtN; i += 256) key[i] = rng[i];
+    if (tid == 0) s_pos = static_cast<int>(rng[kMtN]);
+    __syncthreads();
+    for (int n = 0; n < N; ++n) {
+        const int P = npos[n], Q = nneg[n];
+        const int kp = P < pos_per_image ? P : pos_per_image;
+        int kn = n_sample - kp;
+        kn = Q < kn ? Q : kn;
+        int* out = sample + static_cast<size_t>(n) * n_sample;
+        for (int call = 0; call < 2; ++call) {
+            const int cnt = call == 0 ? P : Q;
+            const int k = call == 0 ? kp : kn;
+            const int off = call == 0 ? 0 : kp;
+            if (cnt == 0) continue;
+            if (wid == 0) {
+                int pos = s_pos;
+                fy_steps_wave(key, pos, cnt - 1, 1, 1, J);  // every step: J[i-1]
+                if (lane_id() == 0) s_pos = pos;
+            }
+            __syncthreads();
+            const int* lst = (call == 0 ? pos_list : neg_list) + static_cast<size_t>(n) * stride;
+            for (int p = tid; p < k; p += 256) {
+                int cur = p;
+                for (int i = (p > 1 ? p : 1); i < cnt; ++i) {
+                    const int j = J[i - 1];
+                    if (cur == i) cur = j;
+                    else if (cur == j) cur = i;
+                }
+                out[off + p] = lst[cur];
+            }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            scount[n] = kp + kn;
+            spos[n] = kp;
+        }
+    }
+    for (int i = tid; i < kMtN; i += 256) rng[i] = key[i];
+    if (tid == 0) rng[kMtN] = static_cast<uint32_t>(s_pos);
+}
+
+// grid N x n_sample: sample_roi, normalised gt_roi_reg and gt_roi_label
+// (utils/utils.py:265-276).  Rows past the sample count are zero.
+struct RegNorm {
+    double mean[4];
+    double stdv[4];
+};
+
+__global__ __launch_bounds__(128) void pt_finish_kernel(
+    int stride, int n_sample, const double* __restrict__ roi_all, const int32_t* __restrict__ assign,
+    const double* __restrict__ gt, const double* __restrict__ gl, const int* __restrict__ gcount,
+    int Gp, const int* __restrict__ sample, const int* __restrict__ scount,
+    const int* __restrict__ spos, RegNorm nrm, double* __restrict__ s_roi, double* __restrict__ s_reg,
+    double* __restrict__ s_lab) {
+    const int n = blockIdx.x;
+    const int s = threadIdx.x + blockIdx.y * 128;
+    if (s >= n_sample) return;
+    const size_t o = static_cast<size_t>(n) * n_sample + s;
+    if (s >= scount[n]) {
+        for (int c = 0; c < 4; ++c) s_roi[o * 4 + c] = s_reg[o * 4 + c] = 0.0;
+        s_lab[o] = 0.0;
+        return;
+    }
+    const int t = sample[o];
+    const double* r = roi_all + (static_cast<size_t>(n) * stride + t) * 4;
+    for (int c = 0; c < 4; ++c) s_roi[o * 4 + c] = r[c];
+    const int G = gcount[n];
+    if (G == 0) {
+        for (int c = 0; c < 4; ++c) s_reg[o * 4 + c] = 0.0;
+        s_lab[o] = 0.0;
+        return;
+    }
+    const int g = assign[static_cast<size_t>(n) * stride + t];
+    const double* b = gt + (static_cast<size_t>(n) * Gp + g) * 4;
+    const double ah = r[2] - r[0], aw = r[3] - r[1];
+    const double acx = (r[2] + r[0]) / 2.0, acy = (r[1] + r[3]) / 2.0;
+    const double bh = b[2] - b[0], bw = b[3] - b[1];
+    const double bcx = (b[2] + b[0]) / 2.0, bcy = (b[1] + b[3]) / 2.0;
+    double v[4];
+    v[0] = (bcx - acx) / ah;
+    v[1] = (bcy - acy) / aw;
+    v[2] = log(bh / ah);
+    v[3] = log(bw / aw);
+    for (int c = 0; c < 4; ++c) s_reg[o * 4 + c] = (v[c] - nrm.mean[c]) / nrm.stdv[c];
+    s_lab[o] = s < spos[n] ? gl[static_cast<size_t>(n) * Gp + g] : 0.0;
+}
+
+// ------------------------------------------------------ generic bbox_iou op
+template <class TA, class TB, class TO>
+__global__ __launch_bounds__(256) void bbox_iou_kernel(const TA* __restrict__ a, int64_t na,
+                                                       const TB* __restrict__ b, int64_t nb,
+                                                       TO* __restrict__ out) {
+    const int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (idx >= na * nb) return;
+    const int64_t i = idx / nb, j = idx - i * nb;
+    const TA* p = a + i * 4;
+    const TB* q = b + j * 4;
+    if (sizeof(TO) == 4) {  // both fp32: numpy computes in fp32
+        float tl0 = np_max<float>(p[0], q[0]), tl1 = np_max<float>(p[1], q[1]);
+        float br0 = np_min<float>(p[2], q[2]), br1 = np_min<float>(p[3], q[3]);
+        float inter = (br0 - tl0) * (br1 - tl1);
+        inter = inter * ((tl0 < br0 && tl1 < br1) ? 1.0f : 0.0f);
+        float aa = area_np(reinterpret_cast<const float*>(p));
+        float ab = area_np(reinterpret_cast<const float*>(q));
+        float uni = aa + ab;
+        uni = uni - inter;
+        out[idx] = static_cast<TO>(inter / uni);
+    } else {
+        const double qa[4] = {static_cast<double>(q[0]), static_cast<double>(q[1]),
+                              static_cast<double>(q[2]), static_cast<double>(q[3])};
+        const double ab = static_cast<double>(area_np(q));
+        out[idx] = static_cast<TO>(iou_np(p, static_cast<double>(area_np(p)), qa, ab));
+    }
+}
+
+// utils/utils.py:75-100 with numpy promotion: anchor statistics in the
+// anchors' dtype, box statistics in the boxes' dtype, result fp64.
+template <class TA, class TB>
+__global__ __launch_bounds__(256) void bbox2reg_kernel(const TA* __restrict__ a,
+                                                       const TB* __restrict__ b, int64_t n,
+                                                       double* __restrict__ out) {
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (i >= n) return;
+    const TA* p = a + i * 4;
+    const TB* q = b + i * 4;
+    const TA ah = p[2] - p[0], aw = p[3] - p[1];
+    const TA acx = (p[2] + p[0]) / TA(2), acy = (p[1] + p[3]) / TA(2);
+    const TB bh = q[2] - q[0], bw = q[3] - q[1];
+    const TB bcx = (q[2] + q[0]) / TB(2), bcy = (q[1] + q[3]) / TB(2);
+    double* o = out + i * 4;
+    if (sizeof(TA) == 4 && sizeof(TB) == 4) {  // both fp32: numpy computes in fp32, stores fp64
+        o[0] = static_cast<double>((bcx - acx) / ah);
+        o[1] = static_cast<double>((bcy - acy) / aw);
+        o[2] = static_cast<double>(logf(static_cast<float>(bh / ah)));
+        o[3] = static_cast<double>(logf(static_cast<float>(bw / aw)));
+    } else {
+        o[0] = (static_cast<double>(bcx) - static_cast<double>(acx)) / static_cast<double>(ah);
+        o[1] = (static_cast<double>(bcy) - static_cast<double>(acy)) / static_cast<double>(aw);
+        o[2] = log(static_cast<double>(bh) / static_cast<double>(ah));
+        o[3] = log(static_cast<double>(bw) / static_cast<double>(aw));
+    }
+}
+
+}  // namespace frcnn
+
+using namespace frcnn;
+
+// =========================================================== C-ABI wrappers
+namespace {
+struct AtWs {
+    double* gt;
+    double* gl;
+    int* gcount;
+    int32_t* row_arg;
+    double* row_max;
+    double* col_v;
+    int* col_i;
+    int8_t* label0;
+    int* pos_list;
+    int* neg_list;
+    int* npos;
+    int* nneg;
+    uint8_t* keep;
+    int* sampled;
+    size_t bytes;
+};
+AtWs carve_at(void* ws, int N, int A, int Gp) {
+    Carver c(ws);
+    AtWs w{};
+    const int nblk = (A + 255) / 256;
+    w.gt = c.take<double>(static_cast<size_t>(N) * Gp * 4);
+    w.gl = c.take<double>(static_cast<size_t>(N) * Gp);
+    w.gcount = c.take<int>(N);
+    w.row_arg = c.take<int32_t>(static_cast<size_t>(N) * A);
+    w.row_max = c.take<double>(static_cast<size_t>(N) * A);
+    w.col_v = c.take<double>(static_cast<size_t>(N) * nblk * Gp);
+    w.col_i = c.take<int>(static_cast<size_t>(N) * nblk * Gp);
+    w.label0 = c.take<int8_t>(static_cast<size_t>(N) * A);
+    w.pos_list = c.take<int>(static_cast<size_t>(N) * A);
+    w.neg_list = c.take<int>(static_cast<size_t>(N) * A);
+    w.npos = c.take<int>(N);
+    w.nneg = c.take<int>(N);
+    w.keep = c.take<uint8_t>(static_cast<size_t>(N) * A);
+    w.sampled = c.take<int>(2 * N);
+    w.bytes = c.used();
+    return w;
+}
+}  // namespace
+
+extern "C" size_t frcnn_anchor_target_workspace_size(int N, int A, int G) {
+    if (N <= 0 || A <= 0 || G < 0) return 0;
+    return carve_at(nullptr, N, A, G > 0 ? G : 1).bytes;
+}
+
+extern "C" int frcnn_anchor_target(int N, int A, int G, const float* anchors, const double* boxes,
+                                   const double* labels, int n_sample, double pos_iou_thresh,
+                                   double neg_iou_thresh, double pos_ratio, uint32_t* rng_state,
+                                   double* reg, int32_t* label, int32_t* argmax, double* max_iou,
+                                   void* workspace, size_t ws_bytes, void* stream) {
+    FRCNN_REQUIRE(N > 0 && N <= 65535 && A > 0 && G >= 0 && G <= kMaxG,
+                  "frcnn_anchor_target: need 0 < N <= 65535, A > 0, 0 <= G <= %d", kMaxG);
+    FRCNN_REQUIRE(anchors && reg && label, "frcnn_anchor_target: null pointer");
+    FRCNN_REQUIRE(G == 0 || (boxes && labels), "frcnn_anchor_target: null boxes");
+    const int n_pos_max = static_cast<int>(pos_ratio * n_sample);  // int(0.5*256) (utils/utils.py:190)
+    FRCNN_REQUIRE(n_sample - (n_pos_max < 0 ? 0 : n_pos_max) <= kMaxKeep && n_pos_max <= kMaxKeep,
+                  "frcnn_anchor_target: n_sample too large");
+    const int Gp = G > 0 ? G : 1;
+    AtWs w = carve_at(workspace, N, A, Gp);
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_anchor_target: workspace %zu < %zu",
+                  ws_bytes, w.bytes);
+    hipStream_t st = as_stream(stream);
+    if (G > 0) {
+        hipLaunchKernelGGL(gt_compact_kernel, dim3(N), dim3(64), 0, st, boxes, labels, G, w.gt, w.gl,
+                           w.gcount);
+        FRCNN_LAUNCH_CHECK("gt_compact_kernel");
+    } else if (hipMemsetAsync(w.gcount, 0, sizeof(int) * N, st) != hipSuccess) {
+        return check_launch("frcnn_anchor_target memset");
+    }
+    const int nblk = (A + 255) / 256;
+    hipLaunchKernelGGL(at_iou_kernel, dim3(nblk, N), dim3(256), 0, st, anchors, A, w.gt, w.gcount,
+                       Gp, w.row_arg, w.row_max, w.col_v, w.col_i);
+    FRCNN_LAUNCH_CHECK("at_iou_kernel");
+    hipLaunchKernelGGL(at_label_kernel, dim3(N), dim3(1024), 0, st, A, Gp, nblk, w.gcount,
+                       w.row_max, w.col_v, w.col_i, neg_iou_thresh, pos_iou_thresh, w.row_arg,
+                       w.label0, w.pos_list, w.neg_list, w.npos, w.nneg);
+    FRCNN_LAUNCH_CHECK("at_label_kernel");
+    if (hipMemsetAsync(w.keep, 0, static_cast<size_t>(N) * A, st) != hipSuccess)
+        return check_launch("frcnn_anchor_target memset");
+    if (rng_state) {
+        hipLaunchKernelGGL(at_sample_kernel, dim3(1), dim3(256), 0, st, N, A, n_sample, n_pos_max,
+                           w.pos_list, w.neg_list, w.npos, w.nneg, rng_state, w.keep, w.sampled);
+        FRCNN_LAUNCH_CHECK("at_sample_kernel");
+    } else if (hipMemsetAsync(w.sampled, 0, sizeof(int) * 2 * N, st) != hipSuccess) {
+        return check_launch("frcnn_anchor_target memset");
+    }
+    hipLaunchKernelGGL(at_finish_kernel, dim3(nblk, N), dim3(256), 0, st, anchors, A, w.gt, w.gcount,
+                       Gp, w.row_arg, w.label0, w.keep, w.sampled, label, reg);
+    FRCNN_LAUNCH_CHECK("at_finish_kernel");
+    if (argmax && hipMemcpyAsync(argmax, w.row_arg, sizeof(int32_t) * N * A,
+                                 hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return check_launch("frcnn_anchor_target copy");
+    if (max_iou && hipMemcpyAsync(max_iou, w.row_max, sizeof(double) * N * A,
+                                  hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return check_launch("frcnn_anchor_target copy");
+    return FRCNN_OK;
+}
+
+namespace {
+struct PtWs {
+    double* gt;
+    double* gl;
+    int* gcount;
+    double* roi_all;
+    int32_t* assign;
+    int* pos_list;
+    int* neg_list;
+    int* npos;
+    int* nneg;
+    int* sample;
+    int* spos;
+    size_t bytes;
+};
+PtWs carve_pt(void* ws, int N, int Rp, int Gp, int n_sample) {
+    Carver c(ws);
+    PtWs w{};
+    const size_t stride = static_cast<size_t>(Rp) + Gp;
+    w.gt = c.take<double>(static_cast<size_t>(N) * Gp * 4);
+    w.gl = c.take<double>(static_cast<size_t>(N) * Gp);
+    w.gcount = c.take<int>(N);
+    w.roi_all = c.take<double>(N * stride * 4);
+    w.assign = c.take<int32_t>(N * stride);
+    w.pos_list = c.take<int>(N * stride);
+    w.neg_list = c.take<int>(N * stride);
+    w.npos = c.take<int>(N);
+    w.nneg = c.take<int>(N);
+    w.sample = c.take<int>(static_cast<size_t>(N) * n_sample);
+    w.spos = c.take<int>(N);
+    w.bytes = c.used();
+    return w;
+}
+}  // namespace
+
+extern "C" size_t frcnn_proposal_target_workspace_size(int N, int Rp, int G, int n_sample) {
+    if (N <= 0 || Rp < 0 || G < 0 || n_sample <= 0) return 0;
+    return carve_pt(nullptr, N, Rp, G > 0 ? G : 1, n_sample).bytes;
+}
+
+extern "C" int frcnn_proposal_target(int N, int Rp, const float* rois, const int32_t* rcount, int G,
+                                     const double* boxes, const double* labels, int n_sample,
+                                     double pos_ratio, double pos_iou_thresh,
+                                     double neg_iou_thresh_high, double neg_iou_thresh_low,
+                                     const double* reg_mean, const double* reg_std,
+                                     uint32_t* rng_state, double* sample_roi, double* gt_roi_reg,
+                                     double* gt_roi_label, int32_t* sample_count, void* workspace,
+                                     size_t ws_bytes, void* stream) {
+    FRCNN_REQUIRE(N > 0 && N <= 65535 && Rp >= 0 && G >= 0 && G <= kMaxG && n_sample > 0,
+                  "frcnn_proposal_target: bad shape");
+    FRCNN_REQUIRE(Rp + G <= kMaxKeep, "frcnn_proposal_target: rois + gt must be <= %d", kMaxKeep);
+    FRCNN_REQUIRE(rcount && rng_state && sample_roi && gt_roi_reg && gt_roi_label && sample_count &&
+                      reg_mean && reg_std,
+                  "frcnn_proposal_target: null pointer");
+    FRCNN_REQUIRE(Rp == 0 || rois, "frcnn_proposal_target: null rois");
+    FRCNN_REQUIRE(G == 0 || (boxes && labels), "frcnn_proposal_target: null boxes");
+    const int Gp = G > 0 ? G : 1;
+    PtWs w = carve_pt(workspace, N, Rp, Gp, n_sample);
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_proposal_target: workspace %zu < %zu",
+                  ws_bytes, w.bytes);
+    hipStream_t st = as_stream(stream);
+    if (G > 0) {
+        hipLaunchKernelGGL(gt_compact_kernel, dim3(N), dim3(64), 0, st, boxes, labels, G, w.gt, w.gl,
+                           w.gcount);
+        FRCNN_LAUNCH_CHECK("gt_compact_kernel");
+    } else if (hipMemsetAsync(w.gcount, 0, sizeof(int) * N, st) != hipSuccess) {
+        return check_launch("frcnn_proposal_target memset");
+    }
+    const int stride = Rp + Gp;
+    hipLaunchKernelGGL(pt_iou_kernel, dim3(N), dim3(1024), 0, st, rois, rcount, Rp, w.gt, w.gl,
+                       w.gcount, Gp, pos_iou_thresh, neg_iou_thresh_high, neg_iou_thresh_low,
+                       w.roi_all, w.assign, w.pos_list, w.neg_list, w.npos, w.nneg);
+    FRCNN_LAUNCH_CHECK("pt_iou_kernel");
+    const int pos_per_image = static_cast<int>(std::nearbyint(n_sample * pos_ratio));  // np.round
+    hipLaunchKernelGGL(pt_sample_kernel, dim3(1), dim3(256), 0, st, N, stride, n_sample,
+                       pos_per_image, w.pos_list, w.neg_list, w.npos, w.nneg, rng_state, w.sample,
+                       sample_count, w.spos);
+    FRCNN_LAUNCH_CHECK("pt_sample_kernel");
+    RegNorm nrm;
+    for (int c = 0; c < 4; ++c) {
+        nrm.mean[c] = reg_mean[c];
+        nrm.stdv[c] = reg_std[c];
+    }
+    hipLaunchKernelGGL(pt_finish_kernel, dim3(N, (n_sample + 127) / 128), dim3(128), 0, st, stride,
+                       n_sample, w.roi_all, w.assign, w.gt, w.gl, w.gcount, Gp, w.sample, sample_count,
+                       w.spos, nrm, sample_roi, gt_roi_reg, gt_roi_label);
+    FRCNN_LAUNCH_CHECK("pt_finish_kernel");
+    return FRCNN_OK;
+}
+
+extern "C" int frcnn_bbox_iou(const void* a, int a_is_f64, int64_t na, const void* b, int b_is_f64,
+                              int64_t nb, void* out, void* stream) {
+    FRCNN_REQUIRE(na >= 0 && nb >= 0, "frcnn_bbox_iou: bad shape");
+    if (na == 0 || nb == 0) return FRCNN_OK;
+    FRCNN_REQUIRE(a && b && out, "frcnn_bbox_iou: null pointer");
+    const int64_t tot = na * nb;
+    dim3 grid(static_cast<unsigned>((tot + 255) / 256));
+    hipStream_t st = as_stream(stream);
+    if (!a_is_f64 && !b_is_f64)
+        hipLaunchKernelGGL((bbox_iou_kernel<float, float, float>), grid, dim3(256), 0, st,
+                           static_cast<const float*>(a), na, static_cast<const float*>(b), nb,
+                           static_cast<float*>(out));
+    else if (!a_is_f64)
+        hipLaunchKernelGGL((bbox_iou_kernel<float, double, double>), grid, dim3(256), 0, st,
+                           static_cast<const float*>(a), na, static_cast<const double*>(b), nb,
+                           static_cast<double*>(out));
+    else if (!b_is_f64)
+        hipLaunchKernelGGL((bbox_iou_kernel<double, float, double>), grid, dim3(256), 0, st,
+                           static_cast<const double*>(a), na, static_cast<const float*>(b), nb,
+                           static_cast<double*>(out));
+    else
+        hipLaunchKernelGGL((bbox_iou_kernel<double, double, double>), grid, dim3(256), 0, st,
+                           static_cast<const double*>(a), na, static_cast<const double*>(b), nb,
+                           static_cast<double*>(out));
+    FRCNN_LAUNCH_CHECK("bbox_iou_kernel");
+    return FRCNN_OK;
+}
+
+extern "C" int frcnn_bbox2reg(const void* anchors, int a_is_f64, const void* bbox, int b_is_f64,
+                              int64_t n, double* out, void* stream) {
+    FRCNN_REQUIRE(n >= 0, "frcnn_bbox2reg: n < 0");
+    if (n == 0) return FRCNN_OK;
+    FRCNN_REQUIRE(anchors && bbox && out, "frcnn_bbox2reg: null pointer");
+    dim3 grid(static_cast<unsigned>((n + 255) / 256));
+    hipStream_t st = as_stream(stream);
+    if (!a_is_f64 && !b_is_f64)
+        hipLaunchKernelGGL((bbox2reg_kernel<float, float>), grid, dim3(256), 0, st,
+                           static_cast<const float*>(anchors), static_cast<const float*>(bbox), n, out);
+    else if (!a_is_f64)
+        hipLaunchKernelGGL((bbox2reg_kernel<float, double>), grid, dim3(256), 0, st,
+                           static_cast<const float*>(anchors), static_cast<const double*>(bbox), n, out);
+    else if (!b_is_f64)
+        hipLaunchKernelGGL((bbox2reg_kernel<double, float>), grid, dim3(256), 0, st,
+                           static_cast<const double*>(anchors), static_cast<const float*>(bbox), n, out);
+    else
+        hipLaunchKernelGGL((bbox2reg_kernel<double, double>), grid, dim3(256), 0, st,
+                           static_cast<const double*>(anchors), static_cast<const double*>(bbox), n, out);
+    FRCNN_LAUNCH_CHECK("bbox2reg_kernel");
+    return FRCNN_OK;
+}

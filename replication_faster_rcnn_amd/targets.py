@@ -1,0 +1,87 @@
+"""Batched target assignment on the HIP path (train.py:67-108 without the
+per-image Python loops).
+
+``anchor_targets`` = AnchorTargetCreator over all images, ``proposal_targets``
+= ProposalTargetCreator over all images.  Both consume numpy's GLOBAL legacy
+RNG exactly like the reference's per-image loops do (all images in order),
+by shipping the MT19937 state to the device and back (one round trip per
+call -- the only host synchronisation).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from .utils import rng_state_from_device, rng_state_to_device
+
+
+def _gt(boxes, labels, dev):
+    b = torch.as_tensor(np.asarray(boxes, np.float64)) if not isinstance(boxes, torch.Tensor) else boxes
+    l = torch.as_tensor(np.asarray(labels, np.float64)) if not isinstance(labels, torch.Tensor) else labels
+    b = b.to(dev, torch.float64).contiguous()
+    l = l.to(dev, torch.float64).contiguous()
+    if b.dim() != 3 or b.size(-1) != 4 or l.shape != b.shape[:2]:
+        raise RuntimeError(f"boxes must be [N,G,4] and labels [N,G]; got {tuple(b.shape)}, {tuple(l.shape)}")
+    return b, l
+
+
+def anchor_targets(boxes, labels, anchors, n_sample=256, pos_iou_thresh=0.7, neg_iou_thresh=0.3,
+                   pos_ratio=0.5, sample=True, internals=False):
+    """boxes [N,G,4] fp64 (label -1 rows = padding), labels [N,G], anchors [A,4]
+    -> reg fp64 [N,A,4], label int32 [N,A] (device tensors)."""
+    lib = _lib.load()
+    dev = _lib.device()
+    b, l = _gt(boxes, labels, dev)
+    a = (anchors if isinstance(anchors, torch.Tensor) else torch.as_tensor(np.asarray(anchors, np.float32)))
+    a = a.to(dev, torch.float32).contiguous()
+    N, G = b.shape[:2]
+    A = a.size(0)
+    reg = torch.empty((N, A, 4), dtype=torch.float64, device=dev)
+    lab = torch.empty((N, A), dtype=torch.int32, device=dev)
+    am = torch.empty((N, A), dtype=torch.int32, device=dev) if internals else None
+    mx = torch.empty((N, A), dtype=torch.float64, device=dev) if internals else None
+    ws = _lib.workspace(lib.frcnn_anchor_target_workspace_size(N, A, G), dev)
+    rng, st = rng_state_to_device(dev) if sample else (None, None)
+    _lib.check(lib.frcnn_anchor_target(N, A, G, _lib.ptr(a), _lib.ptr(b), _lib.ptr(l), int(n_sample),
+                                       float(pos_iou_thresh), float(neg_iou_thresh),
+                                       float(pos_ratio), _lib.ptr(rng), _lib.ptr(reg),
+                                       _lib.ptr(lab), _lib.ptr(am), _lib.ptr(mx), _lib.ptr(ws),
+                                       ws.numel(), _lib.stream_ptr()), "anchor_target")
+    if sample:
+        rng_state_from_device(rng, st)
+    if internals:
+        return reg, lab, am, mx
+    return reg, lab
+
+
+def proposal_targets(rois, rcount, boxes, labels, n_sample=128, pos_ratio=0.5, pos_iou_thresh=0.5,
+                     neg_iou_thresh_high=0.5, neg_iou_thresh_low=0.0,
+                     reg_normalize_mean=(0., 0., 0., 0.), reg_normalize_std=(0.1, 0.1, 0.2, 0.2)):
+    """rois fp32 [N,Rp,4] + rcount int32 [N] -> (sample_roi fp64 [N,S,4],
+    gt_roi_reg fp64 [N,S,4], gt_roi_label fp64 [N,S], count int32 [N])."""
+    lib = _lib.load()
+    dev = _lib.device()
+    b, l = _gt(boxes, labels, dev)
+    r = rois.to(dev, torch.float32).contiguous()
+    c = rcount.to(dev, torch.int32).contiguous()
+    N, G = b.shape[:2]
+    Rp = r.size(1)
+    s_roi = torch.empty((N, n_sample, 4), dtype=torch.float64, device=dev)
+    s_reg = torch.empty((N, n_sample, 4), dtype=torch.float64, device=dev)
+    s_lab = torch.empty((N, n_sample), dtype=torch.float64, device=dev)
+    s_cnt = torch.empty((N,), dtype=torch.int32, device=dev)
+    # utils/utils.py:272 subtracts / divides np.float32 arrays
+    mean = np.asarray(reg_normalize_mean, np.float32).astype(np.float64)
+    std = np.asarray(reg_normalize_std, np.float32).astype(np.float64)
+    ws = _lib.workspace(lib.frcnn_proposal_target_workspace_size(N, Rp, G, n_sample), dev)
+    rng, st = rng_state_to_device(dev)
+    _lib.check(lib.frcnn_proposal_target(N, Rp, _lib.ptr(r), _lib.ptr(c), G, _lib.ptr(b), _lib.ptr(l),
+                                         int(n_sample), float(pos_ratio), float(pos_iou_thresh),
+                                         float(neg_iou_thresh_high), float(neg_iou_thresh_low),
+                                         mean.ctypes.data, std.ctypes.data, _lib.ptr(rng),
+                                         _lib.ptr(s_roi), _lib.ptr(s_reg), _lib.ptr(s_lab),
+                                         _lib.ptr(s_cnt), _lib.ptr(ws), ws.numel(),
+                                         _lib.stream_ptr()), "proposal_target")
+    rng_state_from_device(rng, st)
+    return s_roi, s_reg, s_lab, s_cnt

@@ -1,0 +1,162 @@
+"""Target assignment on the HIP path (utils/utils.py:75-276) vs the golden
+fixtures of the genuine reference and vs the oracle.  Needs an MI355X.
+
+Bars: labels, argmax, sample order and the numpy RNG stream bit-exact;
+max IoU equal as numbers; regression targets within 1e-12 relative (np.log is
+a host SIMD routine, the device uses ocml log; both are ~correctly rounded).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_numpy as orc
+from replication_faster_rcnn_amd import synth, targets
+from replication_faster_rcnn_amd import utils as U
+
+pytestmark = pytest.mark.gpu
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture
+def rng_guard():
+    st = np.random.get_state()
+    yield
+    np.random.set_state(st)
+
+
+def test_bbox_iou_known_answer(golden):
+    g = golden("anchors.npz")
+    out = U.bbox_iou(g["iou_main_a"], g["iou_main_b"])
+    assert np.array_equal(out, g["iou_main_out"])
+    with pytest.raises(IndexError):
+        U.bbox_iou(np.zeros((2, 3)), np.zeros((2, 4)))
+
+
+@pytest.mark.parametrize("da,db", [(np.float32, np.float64), (np.float64, np.float64),
+                                   (np.float32, np.float32), (np.float64, np.float32)])
+def test_bbox_iou_dtypes(da, db):
+    r = np.random.default_rng(2)
+    a = np.concatenate([r.uniform(0, 50, (300, 2)), r.uniform(50, 120, (300, 2))], 1).astype(da)
+    b = np.concatenate([r.uniform(0, 60, (40, 2)), r.uniform(40, 130, (40, 2))], 1).astype(db)
+    a[5] = [3, 3, 3, 3]
+    b[3] = [10, 10, 5, 5]  # inverted box: negative area, -0.0 intersections
+    out = U.bbox_iou(a, b)
+    ref = orc.bbox_iou(a, b)
+    assert out.dtype == ref.dtype
+    np.testing.assert_array_equal(out, ref)
+
+
+def test_bbox2reg_vs_oracle():
+    r = np.random.default_rng(3)
+    a = orc.generate_anchors(orc.generate_anchor_base(), 16, 20, 20)
+    b = np.concatenate([r.uniform(0, 300, (len(a), 2)), r.uniform(300, 600, (len(a), 2))], 1)
+    out = U.bbox2reg(a, b)
+    ref = orc.bbox2reg(a, b)
+    np.testing.assert_array_equal(out[:, :2], ref[:, :2])
+    np.testing.assert_allclose(out[:, 2:], ref[:, 2:], rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("tag", ["small", "train"])
+def test_targets_vs_reference(golden, tag, rng_guard):
+    """The per-image drop-ins, called like train.py:71-108 (all AnchorTarget calls,
+    then all ProposalTarget calls), reproduce the genuine reference's outputs and
+    leave numpy's global RNG in the same state."""
+    g = golden(f"targets_{tag}.npz")
+    anchors, boxes, labels = g["anchors"], g["boxes"], g["labels"]
+    n_img = boxes.shape[0]
+    np.random.set_state(("MT19937", g["rng_key_in"], int(g["rng_pos_in"]), 0, 0.0))
+    at = U.AnchorTargetCreator(256)
+    pt = U.ProposalTargetCreator(128)
+    for i in range(n_img):
+        v = labels[i] != -1
+        reg, lab, am, mx = at(boxes[i, v], anchors, return_internals=True)
+        assert lab.dtype == np.int32
+        assert np.array_equal(lab, g[f"at{i}_label"])
+        assert np.array_equal(am, g[f"at{i}_argmax"])
+        if tag == "small":
+            assert np.array_equal(mx, g[f"at{i}_maxiou"])  # == : -0.0 and 0.0 compare equal
+            if v.sum() == 0:
+                assert reg.dtype == np.float32 and not reg.any()
+            else:
+                np.testing.assert_allclose(reg, g[f"at{i}_reg"], rtol=1e-12, atol=0)
+        else:
+            np.testing.assert_allclose(reg[lab == 1], g[f"at{i}_reg_pos"], rtol=1e-12, atol=0)
+        assert np.random.get_state()[2] == int(g[f"at{i}_rng_pos"])
+        assert sha(np.random.get_state()[1]) == str(g[f"at{i}_rng_key_sha"])
+    for i in range(n_img):
+        v = labels[i] != -1
+        s_roi, s_reg, s_lab = pt(torch.from_numpy(g[f"roi{i}"]), boxes[i, v], labels[i][v])
+        assert np.array_equal(s_roi, g[f"pt{i}_roi"])
+        assert np.array_equal(s_lab, g[f"pt{i}_label"])
+        np.testing.assert_allclose(s_reg, g[f"pt{i}_reg"], rtol=1e-12, atol=1e-15)
+        assert np.random.get_state()[2] == int(g[f"pt{i}_rng_pos"])
+    assert np.array_equal(np.random.get_state()[1], g["rng_key_out"])
+
+
+def test_batched_targets_equal_per_image_loop(rng_guard):
+    """One batched call per stage == the reference's per-image loops (RNG chained
+    across images in order), at the training shape (600x600, 38x38x9, G=32)."""
+    N, G, img = 4, 32, 600
+    anchors = orc.generate_anchors(orc.generate_anchor_base(), 16, 38, 38)
+    bl = [synth.gt_boxes(img, img, G, 21, i, n_valid=[32, 7, 1, 20][i]) for i in range(N)]
+    boxes = np.stack([b for b, _ in bl])
+    labels = np.stack([l for _, l in bl])
+    np.random.seed(77)
+    reg, lab = targets.anchor_targets(boxes, labels, anchors)
+    st_after = np.random.get_state()
+    np.random.seed(77)
+    for i in range(N):
+        v = labels[i] != -1
+        oreg, olab = orc.anchor_target(boxes[i, v], anchors)
+        assert np.array_equal(lab[i].cpu().numpy(), olab)
+        np.testing.assert_allclose(reg[i].cpu().numpy(), oreg, rtol=1e-12, atol=0)
+    assert np.array_equal(np.random.get_state()[1], st_after[1])
+    assert np.random.get_state()[2] == st_after[2]
+    # proposal targets, batched, against the oracle loop
+    rois = []
+    for i in range(N):
+        sc = synth.rpn_scores(len(anchors), 21, i)
+        de = synth.rpn_deltas(len(anchors), 21, i)
+        r, _ = orc.propose_one(anchors, sc, de, img, img, 12000, 600)
+        rois.append(r)
+    Rp = max(len(r) for r in rois)
+    rp = np.zeros((N, Rp, 4), np.float32)
+    for i, r in enumerate(rois):
+        rp[i, :len(r)] = r
+    cnt = torch.tensor([len(r) for r in rois], dtype=torch.int32)
+    np.random.seed(5)
+    s_roi, s_reg, s_lab, s_cnt = targets.proposal_targets(torch.from_numpy(rp), cnt, boxes, labels)
+    st_after = np.random.get_state()
+    np.random.seed(5)
+    for i in range(N):
+        v = labels[i] != -1
+        o_roi, o_reg, o_lab = orc.proposal_target(rois[i], boxes[i, v], labels[i][v])
+        k = int(s_cnt[i])
+        assert k == len(o_roi)
+        assert np.array_equal(s_roi[i, :k].cpu().numpy(), o_roi)
+        assert np.array_equal(s_lab[i, :k].cpu().numpy(), o_lab)
+        np.testing.assert_allclose(s_reg[i, :k].cpu().numpy(), o_reg, rtol=1e-12, atol=1e-15)
+    assert np.array_equal(np.random.get_state()[1], st_after[1])
+
+
+def test_targets_no_gt(rng_guard):
+    anchors = orc.generate_anchors(orc.generate_anchor_base(), 16, 12, 10)
+    np.random.seed(3)
+    reg, lab = U.AnchorTargetCreator()(np.zeros((0, 4)), anchors)
+    st = np.random.get_state()
+    np.random.seed(3)
+    oreg, olab = orc.anchor_target(np.zeros((0, 4)), anchors)
+    assert np.array_equal(lab, olab) and reg.dtype == np.float32 and not reg.any()
+    assert np.array_equal(np.random.get_state()[1], st[1]) and np.random.get_state()[2] == st[2]
+    roi = np.array([[0, 0, 50, 50], [10, 10, 60, 90]], np.float32)
+    np.random.seed(4)
+    out = U.ProposalTargetCreator()(torch.from_numpy(roi), np.zeros((0, 4)), np.zeros(0))
+    np.random.seed(4)
+    ref = orc.proposal_target(roi, np.zeros((0, 4)), np.zeros(0))
+    for a, b in zip(out, ref):
+        assert np.array_equal(a, b)
