@@ -109,15 +109,14 @@ def main():
     world, rank, local = setup_dist(args.gpus)
     dev = torch.device("cuda", local)
     from replication_faster_rcnn_amd import anchors as A, ops
-    c, sc, de, x = make_inputs(args.config, c_batch(args.config), rank * c_batch(args.config), dev)
+    from replication_faster_rcnn_amd import dist as fdist
+    per_rank = c_batch(args.config)
+    mine = fdist.shard(per_rank * world, rank, world)  # weak scaling: per_rank images per GPU
+    c, sc, de, x = make_inputs(args.config, len(mine), mine.start, dev)
     N = sc.size(0)
     base = A.generate_anchor_base_device(anchor_scales=c["scales"])
     post = c["post_nms"]
     inds = torch.arange(N, device=dev, dtype=torch.float32).repeat_interleave(post)
-    if world > 1:
-        g_rois = torch.empty((world * N, post, 4), device=dev)
-        g_idx = torch.empty((world * N, post), dtype=torch.int32, device=dev)
-        g_cnt = torch.empty((world * N,), dtype=torch.int32, device=dev)
     ev = []
 
     def step(timed):
@@ -129,14 +128,12 @@ def main():
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        pooled, am = ops._roi_pool_fwd(x, boxes, 7, 7, 1.0)
+        pooled, am = ops._roi_pool_fwd(x, boxes, 7, 7, 1.0, rois_sorted=True)
         if timed:
             e1.record()
             ev.append((e0, e1))
-        if world > 1:
-            dist.all_gather_into_tensor(g_rois, rois)
-            dist.all_gather_into_tensor(g_idx, idx)
-            dist.all_gather_into_tensor(g_cnt, cnt)
+        if world > 1:  # the only collective: detections of all ranks (RCCL over xGMI)
+            fdist.all_gather_detections(rois, idx, cnt)
         return cnt
 
     for _ in range(args.warmup):

@@ -334,20 +334,75 @@ __global__ __launch_bounds__(kTileThreads) void roi_pool_fwd_wave_kernel(
 // Pixel-major variant: the LDS tile is [H*W][8] (8 channels of one pixel are
 // 32 contiguous bytes), so a lane reads its bin pixel for all 8 channels with
 // two ds_read_b128 from a single address -- no per-channel address math.
+// Count of RoIs with batch index < b0 and < b1 (block-wide), for RoIs grouped by
+// non-decreasing batch index: image b's RoIs are then [count(<b), count(<b+1)).
 template <int NT>
+__device__ __forceinline__ int2 roi_range_sorted(const float* __restrict__ rois, int R, int b0,
+                                                 int b1, int* red) {
+    int c0 = 0, c1 = 0;
+    for (int r = threadIdx.x; r < R; r += NT) {
+        const int rb = static_cast<int>(rois[static_cast<size_t>(r) * 5]);
+        c0 += rb < b0;
+        c1 += rb < b1;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        c0 += __shfl_xor(c0, o, 64);
+        c1 += __shfl_xor(c1, o, 64);
+    }
+    const int wid = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[2 * wid] = c0;
+        red[2 * wid + 1] = c1;
+    }
+    __syncthreads();
+    int2 res = make_int2(0, 0);
+    for (int w = 0; w < NT / 64; ++w) {
+        res.x += red[2 * w];
+        res.y += red[2 * w + 1];
+    }
+    return res;
+}
+
+// SORTED: RoIs grouped by non-decreasing batch index (no list kernel, no fill
+// kernel: grid row y == N writes 0 / -1 for RoIs whose index is outside [0, N)).
+template <int NT, bool SORTED>
 __global__ __launch_bounds__(NT) void roi_pool_fwd_px8_kernel(
     const float* __restrict__ x, const float* __restrict__ rois, const int* __restrict__ list,
     const int* __restrict__ cnt, int* __restrict__ queue, int R, int C, int H, int W, int PH,
     int PW, float ss, float* __restrict__ out, int32_t* __restrict__ argmax) {
     constexpr int CG = 8;
     extern __shared__ __attribute__((aligned(16))) float4 tile4[];  // [H*W][2] float4
+    __shared__ int s_red[2 * (NT / 64)];
     const int b = blockIdx.y;
     const int c0 = blockIdx.x * CG;
     const int tid = threadIdx.x, lane = tid & 63;
     const int HW = H * W;
     const int PHW = PH * PW;
-    const int nr = cnt[b];
     const int split = gridDim.z;
+    int nr, rbase = 0;
+    if (SORTED) {
+        const int N = gridDim.y - 1;
+        if (b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
+            const int2 rg = roi_range_sorted<NT>(rois, R, 0, N, s_red);
+            const int n_lo = rg.x, n_hi = R - rg.y, tot = n_lo + n_hi;
+            const int lo = static_cast<int>(static_cast<int64_t>(tot) * blockIdx.z / split);
+            const int hi = static_cast<int>(static_cast<int64_t>(tot) * (blockIdx.z + 1) / split);
+            for (int e = lo * CG * PHW + tid; e < hi * CG * PHW; e += NT) {
+                const int t = e / (CG * PHW);
+                const int rem = e - t * (CG * PHW);
+                const int r = t < n_lo ? t : rg.y + (t - n_lo);
+                const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + rem;
+                out[o] = 0.0f;
+                argmax[o] = -1;
+            }
+            return;
+        }
+        const int2 rg = roi_range_sorted<NT>(rois, R, b, b + 1, s_red);
+        rbase = rg.x;
+        nr = rg.y - rg.x;
+    } else {
+        nr = cnt[b];
+    }
     const int r_begin = static_cast<int>(static_cast<int64_t>(nr) * blockIdx.z / split);
     const int r_end = static_cast<int>(static_cast<int64_t>(nr) * (blockIdx.z + 1) / split);
     if (r_begin >= r_end) return;
@@ -362,7 +417,7 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_px8_kernel(
         tile[p * CG + qq] = src[i];
     }
     __syncthreads();
-    const int* lst = list + static_cast<size_t>(b) * R;
+    const int* lst = SORTED ? nullptr : list + static_cast<size_t>(b) * R;
     const int ph = lane / PW, pw = lane - (lane / PW) * PW;
     const bool act = lane < PHW;
     int t = 0;
@@ -371,7 +426,7 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_px8_kernel(
     while (t < r_end) {
         int tn = 0;
         if (lane == 0) tn = atomicAdd(&s_next, 1);  // prefetch the next item
-        const int r = __builtin_amdgcn_readfirstlane(lst[t]);
+        const int r = SORTED ? rbase + t : __builtin_amdgcn_readfirstlane(lst[t]);
         const RoiGeom gm = roi_geom(rois + static_cast<size_t>(r) * 5, ss, PH, PW);
         int4 g = geom_bin(gm, H, W, ph, pw);
         if (!act) g = make_int4(0, 0, 0, 0);
@@ -823,13 +878,13 @@ extern "C" size_t frcnn_roi_pool_fwd_workspace_size(int64_t R, int N, int C) {
 }
 
 extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, int N, int C,
-                                  int H, int W, int PH, int PW, float spatial_scale, float* out,
-                                  int32_t* argmax, void* workspace, size_t ws_bytes,
-                                  void* stream) {
+                                  int H, int W, int PH, int PW, float spatial_scale,
+                                  int rois_sorted, float* out, int32_t* argmax, void* workspace,
+                                  size_t ws_bytes, void* stream) {
     FRCNN_REQUIRE(R >= 0 && N >= 0 && C >= 0 && H >= 0 && W >= 0, "frcnn_roi_pool_fwd: bad shape");
     FRCNN_REQUIRE(PH > 0 && PW > 0 && PH * PW <= kMaxBins,
                   "frcnn_roi_pool_fwd: output_size must have 1..%d bins", kMaxBins);
-    FRCNN_REQUIRE(R <= 0x7fffffff && N <= 65535, "frcnn_roi_pool_fwd: too many rois / images");
+    FRCNN_REQUIRE(R <= 0x7fffffff && N <= 65534, "frcnn_roi_pool_fwd: too many rois / images");
     if (R == 0 || C == 0) return FRCNN_OK;
     FRCNN_REQUIRE(x && rois && out && argmax, "frcnn_roi_pool_fwd: null pointer");
     hipStream_t st = as_stream(stream);
@@ -837,6 +892,21 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
     const size_t tile_bytes = kFwdCG * HW * sizeof(float);
     const bool aligned = (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
                          (reinterpret_cast<uintptr_t>(argmax) % 16 == 0);
+    const char* var = getenv("FRCNN_ROIPOOL_VARIANT");  // A/B override (tests, tools/ab_roi_pool.py)
+    const bool px8_ok = N > 0 && HW > 0 && C % 8 == 0 && 2 * tile_bytes <= kFwdTileBudget &&
+                        PH * PW <= 64;
+    const int64_t per_img = (R + (N > 0 ? N : 1) - 1) / (N > 0 ? N : 1);
+    int64_t split8 = px8_ok ? (512 + static_cast<int64_t>(C / 8) * N - 1) / (static_cast<int64_t>(C / 8) * N) : 1;
+    split8 = split8 < 1 ? 1 : (split8 > 64 ? 64 : split8);
+    // default: one launch (px8, 16-wave workgroups) when the RoIs are grouped by image
+    if (px8_ok && rois_sorted && !var) {
+        dim3 grid(C / 8, N + 1, static_cast<unsigned>(split8));
+        hipLaunchKernelGGL((roi_pool_fwd_px8_kernel<1024, true>), grid, dim3(1024), 2 * tile_bytes, st,
+                           x, rois, nullptr, nullptr, nullptr, static_cast<int>(R), C, H, W, PH, PW,
+                           spatial_scale, out, argmax);
+        FRCNN_LAUNCH_CHECK("roi_pool_fwd_px8_kernel");
+        return FRCNN_OK;
+    }
     if (N > 0 && C % kFwdCG == 0 && HW > 0 && tile_bytes <= kFwdTileBudget && aligned) {
         FwdWs w = carve_fwd(workspace, R, N, C);
         FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_fwd: workspace %zu < %zu",
@@ -845,61 +915,53 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
                            static_cast<int>(R), N, w.list, w.cnt, w.queue, C / 4);
         FRCNN_LAUNCH_CHECK("roi_lists_kernel");
         const int groups = C / kFwdCG;
-        const int64_t per_img = (R + N - 1) / N;
         int64_t split = (1024 + static_cast<int64_t>(groups) * N - 1) / (static_cast<int64_t>(groups) * N);
         int64_t cap = (per_img + 31) / 32;
         split = split < cap ? split : cap;
         split = split < 1 ? 1 : (split > 64 ? 64 : split);
-        // px8: 8-channel groups, >= 2 workgroups per CU, all sharing one queue per group
-        int64_t split8 = (512 + static_cast<int64_t>(C / 8) * N - 1) / (static_cast<int64_t>(C / 8) * N);
-        split8 = split8 < 1 ? 1 : (split8 > 64 ? 64 : split8);
-        const char* var = getenv("FRCNN_ROIPOOL_VARIANT");  // A/B override: tile | wave4 | wave8
-        const bool wave_ok = PH * PW <= 64;
-        if (wave_ok && !(var && var[0] == 't')) {
-            const size_t pad = 8 * sizeof(float);
-            if (var && std::strcmp(var, "pxf8") == 0 && C % 8 == 0 && 2 * tile_bytes + pad <= kFwdTileBudget) {
-                dim3 grid(C / 8, N, static_cast<unsigned>(split8));
-                hipLaunchKernelGGL(roi_pool_fwd_pxf_kernel<8>, grid, dim3(kTileThreads), 2 * tile_bytes + pad, st,
-                                   x, rois, w.list, w.cnt, static_cast<int>(R), C, H, W, PH, PW,
-                                   spatial_scale, out, argmax);
-            } else if (var && std::strcmp(var, "pxf4") == 0) {
-                dim3 grid(C / 4, N, static_cast<unsigned>(split));
-                hipLaunchKernelGGL(roi_pool_fwd_pxf_kernel<4>, grid, dim3(kTileThreads), tile_bytes + pad, st,
-                                   x, rois, w.list, w.cnt, static_cast<int>(R), C, H, W, PH, PW,
-                                   spatial_scale, out, argmax);
-            } else if (var && std::strcmp(var, "px8s") == 0 && C % 8 == 0 && 2 * tile_bytes <= kFwdTileBudget) {
-                dim3 grid(C / 8, N, static_cast<unsigned>(split));
-                hipLaunchKernelGGL(roi_pool_fwd_px8s_kernel, grid, dim3(kTileThreads), 2 * tile_bytes, st,
-                                   x, rois, w.list, w.cnt, static_cast<int>(R), C, H, W, PH, PW,
-                                   spatial_scale, out, argmax);
-            } else if (var && std::strcmp(var, "px8") == 0 && C % 8 == 0 && 2 * tile_bytes <= kFwdTileBudget) {
-                dim3 grid(C / 8, N, static_cast<unsigned>(split8));
-                hipLaunchKernelGGL(roi_pool_fwd_px8_kernel<512>, grid, dim3(512), 2 * tile_bytes, st,
-                                   x, rois, w.list, w.cnt, w.queue, static_cast<int>(R), C, H, W, PH, PW,
-                                   spatial_scale, out, argmax);
-            } else if (!(var && var[0] == 'w') && C % 8 == 0 && 2 * tile_bytes <= kFwdTileBudget) {
-                // default: 16-wave workgroups, two per CU share-nothing (2 x 77 KB LDS at 38x63)
-                dim3 grid(C / 8, N, static_cast<unsigned>(split8));
-                hipLaunchKernelGGL(roi_pool_fwd_px8_kernel<1024>, grid, dim3(1024), 2 * tile_bytes, st,
-                                   x, rois, w.list, w.cnt, w.queue, static_cast<int>(R), C, H, W, PH, PW,
-                                   spatial_scale, out, argmax);
-            } else if (var && std::strcmp(var, "wave8") == 0 && C % 8 == 0 && 2 * tile_bytes <= kFwdTileBudget) {
-                dim3 grid(C / 8, N, static_cast<unsigned>(split));
-                hipLaunchKernelGGL(roi_pool_fwd_wave_kernel<8>, grid, dim3(kTileThreads), 2 * tile_bytes, st,
-                                   x, rois, w.list, w.cnt, static_cast<int>(R), C, H, W, PH, PW,
-                                   spatial_scale, out, argmax);
-            } else {
-                hipLaunchKernelGGL(roi_pool_fwd_wave_kernel<4>, dim3(groups, N, static_cast<unsigned>(split)),
-                                   dim3(kTileThreads), tile_bytes, st, x, rois, w.list, w.cnt,
-                                   static_cast<int>(R), C, H, W, PH, PW, spatial_scale, out, argmax);
-            }
-            FRCNN_LAUNCH_CHECK("roi_pool_fwd_wave_kernel");
+        const size_t pad = 8 * sizeof(float);
+        auto is = [&](const char* v) { return var && std::strcmp(var, v) == 0; };
+        if (px8_ok && !(var && var[0] == 'w') && !is("tile") && !is("px8s") && !is("pxf8") &&
+            !is("pxf4") && !is("px8")) {
+            dim3 grid(C / 8, N, static_cast<unsigned>(split8));  // default (unsorted RoIs)
+            hipLaunchKernelGGL((roi_pool_fwd_px8_kernel<1024, false>), grid, dim3(1024), 2 * tile_bytes,
+                               st, x, rois, w.list, w.cnt, w.queue, static_cast<int>(R), C, H, W, PH,
+                               PW, spatial_scale, out, argmax);
+        } else if (px8_ok && is("px8")) {
+            dim3 grid(C / 8, N, static_cast<unsigned>(split8));
+            hipLaunchKernelGGL((roi_pool_fwd_px8_kernel<512, false>), grid, dim3(512), 2 * tile_bytes,
+                               st, x, rois, w.list, w.cnt, w.queue, static_cast<int>(R), C, H, W, PH,
+                               PW, spatial_scale, out, argmax);
+        } else if (px8_ok && is("px8s")) {
+            dim3 grid(C / 8, N, static_cast<unsigned>(split8));
+            hipLaunchKernelGGL(roi_pool_fwd_px8s_kernel, grid, dim3(kTileThreads), 2 * tile_bytes, st,
+                               x, rois, w.list, w.cnt, static_cast<int>(R), C, H, W, PH, PW,
+                               spatial_scale, out, argmax);
+        } else if (px8_ok && is("pxf8") && 2 * tile_bytes + pad <= kFwdTileBudget) {
+            dim3 grid(C / 8, N, static_cast<unsigned>(split8));
+            hipLaunchKernelGGL(roi_pool_fwd_pxf_kernel<8>, grid, dim3(kTileThreads), 2 * tile_bytes + pad,
+                               st, x, rois, w.list, w.cnt, static_cast<int>(R), C, H, W, PH, PW,
+                               spatial_scale, out, argmax);
+        } else if (PH * PW <= 64 && is("pxf4")) {
+            dim3 grid(groups, N, static_cast<unsigned>(split));
+            hipLaunchKernelGGL(roi_pool_fwd_pxf_kernel<4>, grid, dim3(kTileThreads), tile_bytes + pad, st,
+                               x, rois, w.list, w.cnt, static_cast<int>(R), C, H, W, PH, PW,
+                               spatial_scale, out, argmax);
+        } else if (PH * PW <= 64 && is("wave8") && C % 8 == 0 && 2 * tile_bytes <= kFwdTileBudget) {
+            dim3 grid(C / 8, N, static_cast<unsigned>(split));
+            hipLaunchKernelGGL(roi_pool_fwd_wave_kernel<8>, grid, dim3(kTileThreads), 2 * tile_bytes, st,
+                               x, rois, w.list, w.cnt, static_cast<int>(R), C, H, W, PH, PW,
+                               spatial_scale, out, argmax);
+        } else if (PH * PW <= 64 && !is("tile")) {
+            hipLaunchKernelGGL(roi_pool_fwd_wave_kernel<4>, dim3(groups, N, static_cast<unsigned>(split)),
+                               dim3(kTileThreads), tile_bytes, st, x, rois, w.list, w.cnt,
+                               static_cast<int>(R), C, H, W, PH, PW, spatial_scale, out, argmax);
         } else {
             hipLaunchKernelGGL(roi_pool_fwd_tile_kernel, dim3(groups, N, static_cast<unsigned>(split)),
-                               dim3(kTileThreads), tile_bytes, st, x, rois, w.list, w.cnt, static_cast<int>(R), C,
-                               H, W, PH, PW, kFwdCG, spatial_scale, out, argmax);
-            FRCNN_LAUNCH_CHECK("roi_pool_fwd_tile_kernel");
+                               dim3(kTileThreads), tile_bytes, st, x, rois, w.list, w.cnt,
+                               static_cast<int>(R), C, H, W, PH, PW, kFwdCG, spatial_scale, out, argmax);
         }
+        FRCNN_LAUNCH_CHECK("roi_pool_fwd (image tile)");
         hipLaunchKernelGGL(roi_pool_invalid_fill_kernel, dim3(64), dim3(256), 0, st, w.list, w.cnt,
                            static_cast<int>(R), N, static_cast<size_t>(C) * PH * PW, out, argmax);
         FRCNN_LAUNCH_CHECK("roi_pool_invalid_fill_kernel");

@@ -27,10 +27,16 @@ class ResnetHead(nn.Module):
         """-> (cls [N, n_classes, n_sample], reg [N, n_sample, n_classes*4])."""
         N = x.shape[0]
         dev = _lib.device()
+        ri_in = torch.as_tensor(roi_inds).detach()
+        sorted_inds = None
+        if not ri_in.is_cuda:  # train.py builds roi_inds on the host, grouped by image
+            bi = ri_in.to(torch.int64)
+            sorted_inds = bool((bi[1:] >= bi[:-1]).all()) if bi.numel() > 1 else True
         r = torch.as_tensor(rois).detach().to(dev, torch.float32).contiguous()
-        ri = torch.as_tensor(roi_inds).detach().to(dev, torch.float32).contiguous()
+        ri = ri_in.to(dev, torch.float32).contiguous()
         boxes = ops.roi_transform(r, ri, img_h, img_w, x.shape[2], x.shape[3])
-        cropped = ops.roi_pool(x, boxes, (self.roi_size, self.roi_size), self.spatial_scale)
+        cropped = ops.roi_pool(x, boxes, (self.roi_size, self.roi_size), self.spatial_scale,
+                               rois_sorted=sorted_inds)
         fc6 = self.classifier(cropped)
         fc6 = fc6.view(fc6.shape[0], -1)
         reg = self.reg(fc6)

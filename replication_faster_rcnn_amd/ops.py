@@ -48,17 +48,30 @@ def nms(boxes: torch.Tensor, scores: torch.Tensor, iou_threshold: float) -> torc
 
 
 # ------------------------------------------------------------------ roi_pool
-def _roi_pool_fwd(x: torch.Tensor, rois: torch.Tensor, ph: int, pw: int, ss: float):
+def _roi_pool_fwd(x: torch.Tensor, rois: torch.Tensor, ph: int, pw: int, ss: float,
+                  rois_sorted: bool = False):
     lib = _lib.load()
     N, C, H, W = x.shape
     R = rois.size(0)
     out = torch.empty((R, C, ph, pw), dtype=torch.float32, device=x.device)
     am = torch.empty((R, C, ph, pw), dtype=torch.int32, device=x.device)
-    ws = _lib.workspace(lib.frcnn_roi_pool_fwd_workspace_size(R, N, C), x.device)
+    ws = None if rois_sorted else _lib.workspace(lib.frcnn_roi_pool_fwd_workspace_size(R, N, C),
+                                                 x.device)
     _lib.check(lib.frcnn_roi_pool_fwd(_lib.ptr(x), _lib.ptr(rois), R, N, C, H, W, ph, pw, float(ss),
-                                      _lib.ptr(out), _lib.ptr(am), _lib.ptr(ws), ws.numel(),
+                                      int(bool(rois_sorted)), _lib.ptr(out), _lib.ptr(am),
+                                      _lib.ptr(ws), 0 if ws is None else ws.numel(),
                                       _lib.stream_ptr()), "roi_pool forward")
     return out, am
+
+
+def _sorted_by_image(boxes) -> bool:
+    """Host-side check when the RoIs live on the host (the reference's case);
+    device RoIs are treated as unsorted unless the caller says otherwise."""
+    if isinstance(boxes, torch.Tensor) and boxes.is_cuda:
+        return False
+    b = (boxes.detach() if isinstance(boxes, torch.Tensor) else torch.as_tensor(boxes))[:, 0]
+    bi = b.to(torch.int64)
+    return bool((bi[1:] >= bi[:-1]).all()) if bi.numel() > 1 else True
 
 
 def _roi_pool_bwd(grad: torch.Tensor, rois: torch.Tensor, am: torch.Tensor, shape, ss: float):
@@ -75,8 +88,8 @@ def _roi_pool_bwd(grad: torch.Tensor, rois: torch.Tensor, am: torch.Tensor, shap
 
 class _RoIPoolFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, rois, ph, pw, ss):
-        out, am = _roi_pool_fwd(x, rois, ph, pw, ss)
+    def forward(ctx, x, rois, ph, pw, ss, rois_sorted=False):
+        out, am = _roi_pool_fwd(x, rois, ph, pw, ss, rois_sorted)
         ctx.save_for_backward(rois, am)
         ctx.meta = (tuple(x.shape), ss)
         ctx.mark_non_differentiable(am)
@@ -87,7 +100,7 @@ class _RoIPoolFunction(torch.autograd.Function):
         rois, am = ctx.saved_tensors
         shape, ss = ctx.meta
         gi = _roi_pool_bwd(grad_out.contiguous().float(), rois, am, shape, ss)
-        return gi, None, None, None, None
+        return gi, None, None, None, None, None
 
 
 def _boxes_to_rois(boxes: Union[torch.Tensor, List[torch.Tensor]]) -> torch.Tensor:
@@ -100,22 +113,29 @@ def _boxes_to_rois(boxes: Union[torch.Tensor, List[torch.Tensor]]) -> torch.Tens
     return boxes
 
 
-def roi_pool_with_argmax(input: torch.Tensor, boxes, output_size, spatial_scale: float = 1.0
-                         ) -> Tuple[torch.Tensor, torch.Tensor]:
-    """roi_pool returning (out, argmax int32) -- the torch.ops.torchvision.roi_pool pair."""
+def roi_pool_with_argmax(input: torch.Tensor, boxes, output_size, spatial_scale: float = 1.0,
+                         rois_sorted=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """roi_pool returning (out, argmax int32) -- the torch.ops.torchvision.roi_pool pair.
+    ``rois_sorted``: RoIs grouped by non-decreasing batch index (None = check
+    host-resident RoIs, assume unsorted for device RoIs)."""
     if input.dim() != 4:
         raise RuntimeError("input must be [N, C, H, W]")
     ph, pw = (output_size, output_size) if isinstance(output_size, int) else tuple(output_size)
     out_dev = input.device
     x = _to_dev(input)  # differentiable move, so CPU leaf tensors get their grad
-    rois = _to_dev(_boxes_to_rois(boxes))
-    out, am = _RoIPoolFunction.apply(x.contiguous(), rois, int(ph), int(pw), float(spatial_scale))
+    b = _boxes_to_rois(boxes)
+    if rois_sorted is None:
+        rois_sorted = _sorted_by_image(b)
+    rois = _to_dev(b)
+    out, am = _RoIPoolFunction.apply(x.contiguous(), rois, int(ph), int(pw), float(spatial_scale),
+                                     bool(rois_sorted))
     return out.to(out_dev), am.to(out_dev)
 
 
-def roi_pool(input: torch.Tensor, boxes, output_size, spatial_scale: float = 1.0) -> torch.Tensor:
+def roi_pool(input: torch.Tensor, boxes, output_size, spatial_scale: float = 1.0,
+             rois_sorted=None) -> torch.Tensor:
     """torchvision.ops.roi_pool (nets/heads.py:48)."""
-    return roi_pool_with_argmax(input, boxes, output_size, spatial_scale)[0]
+    return roi_pool_with_argmax(input, boxes, output_size, spatial_scale, rois_sorted)[0]
 
 
 # ------------------------------------------------------------------ proposals

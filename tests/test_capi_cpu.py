@@ -48,7 +48,7 @@ def test_argument_validation_without_gpu():
     """Shape errors are reported before any HIP call (rc=-1 + message)."""
     from replication_faster_rcnn_amd import _lib
     lib = _lib.load(require_gpu=False)
-    rc = lib.frcnn_roi_pool_fwd(None, None, 1, 1, 1, 1, 1, 0, 7, 1.0, None, None, None, 0, None)
+    rc = lib.frcnn_roi_pool_fwd(None, None, 1, 1, 1, 1, 1, 0, 7, 1.0, 0, None, None, None, 0, None)
     assert rc == -1 and b"output_size" in lib.frcnn_last_error()
     p = _lib.ProposeParams()
     assert lib.frcnn_propose_workspace_size(ctypes.byref(p)) == 0  # N=0 rejected

@@ -193,13 +193,14 @@ def test_roi_pool_bwd_deterministic():
     assert torch.equal(a, b)
 
 
-def test_roi_pool_out_of_range_batch_index():
+@pytest.mark.parametrize("sorted_", [False, True])
+def test_roi_pool_out_of_range_batch_index(sorted_):
     """Extension: RoIs whose batch index is outside [0, N) pool to 0 / -1
     (torchvision reads out of bounds there)."""
     x = torch.randn(2, 8, 10, 12, device=DEV)
     rois = torch.tensor([[-1, 0, 0, 5, 5], [1, 0, 0, 9, 9], [2, 1, 1, 4, 4], [7, 0, 0, 3, 3]],
                         dtype=torch.float32, device=DEV)
-    out, am = ops.roi_pool_with_argmax(x, rois, 7)
+    out, am = ops.roi_pool_with_argmax(x, rois, 7, rois_sorted=sorted_)
     assert (out[[0, 2, 3]] == 0).all() and (am[[0, 2, 3]] == -1).all()
     oo, oa = orc.roi_pool_forward(x.cpu().numpy(), rois[1:2].cpu().numpy(), 7, 1.0)
     assert np.array_equal(out[1:2].cpu().numpy(), oo) and np.array_equal(am[1:2].cpu().numpy(), oa)
@@ -266,10 +267,15 @@ def test_roi_pool_special_values(variant, monkeypatch):
     assert np.array_equal(out.cpu().numpy().view(np.uint32), oo.view(np.uint32))
 
 
-@pytest.mark.parametrize("variant", ["px8w16", "px8s", "px8", "pxf8", "pxf4", "wave8", "wave4", "tile"])
+@pytest.mark.parametrize("variant", ["sorted", "px8w16", "px8s", "px8", "pxf8", "pxf4", "wave8",
+                                     "wave4", "tile"])
 def test_roi_pool_variants_random(variant, monkeypatch):
-    """Every forward variant, cfg2-like random RoIs, bit-exact vs the oracle."""
-    monkeypatch.setenv("FRCNN_ROIPOOL_VARIANT", variant)
+    """Every forward variant, cfg2-like random RoIs, bit-exact vs the oracle
+    ("sorted" = the default single-launch path for RoIs grouped by image)."""
+    if variant == "sorted":
+        monkeypatch.delenv("FRCNN_ROIPOOL_VARIANT", raising=False)
+    else:
+        monkeypatch.setenv("FRCNN_ROIPOOL_VARIANT", variant)
     r = np.random.default_rng(11)
     N, C, H, W, R = 3, 32, 38, 63, 600
     x = r.standard_normal((N, C, H, W), dtype=np.float32)
@@ -278,7 +284,8 @@ def test_roi_pool_variants_random(variant, monkeypatch):
     xy = r.uniform(-3, 60, (R, 2)).astype(np.float32)
     wh = r.uniform(0, 40, (R, 2)).astype(np.float32)
     rois = np.concatenate([b[:, None], xy, xy + wh], 1).astype(np.float32)
-    out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7)
+    out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7,
+                                       rois_sorted=(variant == "sorted"))
     oo, oa = orc.roi_pool_forward(x, rois, 7)
     assert np.array_equal(am.cpu().numpy(), oa)
     assert np.array_equal(out.cpu().numpy(), oo)

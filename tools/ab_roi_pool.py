@@ -21,7 +21,7 @@ from replication_faster_rcnn_amd import anchors as A, ops, synth  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg2")
-    ap.add_argument("--variants", default="wave4,wave8,tile")
+    ap.add_argument("--variants", default="sorted,px8w16,px8")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
@@ -43,8 +43,12 @@ def main():
     times = {v: [] for v in variants}
     for rnd in range(a.rounds):
         for v in variants:
-            os.environ["FRCNN_ROIPOOL_VARIANT"] = v
-            out, am = ops._roi_pool_fwd(x, boxes, 7, 7, 1.0)
+            srt = v == "sorted"  # the default single-launch path (proposals are grouped by image)
+            if srt:
+                os.environ.pop("FRCNN_ROIPOOL_VARIANT", None)
+            else:
+                os.environ["FRCNN_ROIPOOL_VARIANT"] = v
+            out, am = ops._roi_pool_fwd(x, boxes, 7, 7, 1.0, srt)
             if ref is None:
                 ref = (out.clone(), am.clone())
             elif rnd == 0:
@@ -52,7 +56,7 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.iters):
-                ops._roi_pool_fwd(x, boxes, 7, 7, 1.0)
+                ops._roi_pool_fwd(x, boxes, 7, 7, 1.0, srt)
             e1.record()
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1) / a.iters * 1e3)

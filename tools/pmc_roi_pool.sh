@@ -2,7 +2,7 @@
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=${1:-gpurun_out/pmc}
-VAR=${2:-px8}
+VAR=${2:-sorted}
 CFG=${3:-cfg2}
 mkdir -p "$OUT"
 run() {  # name counters...
