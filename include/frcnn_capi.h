@@ -105,9 +105,10 @@ int frcnn_roi_transform(const float* rois, const float* roi_inds, int64_t R, flo
  *   x fp32 [N,C,H,W], rois fp32 [R,5] -> out fp32 [R,C,PH,PW],
  *   argmax int32 [R,C,PH,PW] (h*W+w within the plane, -1 for empty bins).
  * RoIs whose batch index is outside [0,N) produce 0 / -1.
- * rois_sorted != 0 promises the RoIs are grouped by non-decreasing batch index
- * (true for proposals and for train.py's sample_rois_ind): one kernel launch,
- * no workspace used. */
+ * rois_sorted != 0 says the RoIs are grouped by batch index (true for
+ * proposals and for train.py's sample_rois_ind): a cost-balanced two-launch
+ * path (partition + pool); the result is exact for any order either way.
+ * The workspace (frcnn_roi_pool_fwd_workspace_size bytes) is always required. */
 size_t frcnn_roi_pool_fwd_workspace_size(int64_t R, int N, int C);
 int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
                        int PH, int PW, float spatial_scale, int rois_sorted, float* out,

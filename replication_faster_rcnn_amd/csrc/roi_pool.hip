@@ -466,6 +466,466 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_px8_kernel(
     }
 }
 
+// ---------------------------------------------------- cost-balanced forward
+// Work estimate of one RoI for the wave-per-RoI loop below: the wave's pixel
+// loop runs (max bin-window height) x (max bin-window width) iterations --
+// about floor(bin size) + 2 each way, at most the RoI's visible extent -- plus
+// a fixed part (geometry, 2*CG stores).  A RoI with an out-of-range batch
+// index, or entirely outside the map, only stores.
+__device__ __forceinline__ int roi_cost_fast(const float* __restrict__ rois, int t, float ss, int N, int H,
+                                             int W, int PH, int PW) {
+    const float* roi = rois + static_cast<size_t>(t) * 5;
+    const int b = static_cast<int>(roi[0]);
+    const int sw = static_cast<int>(roundf(roi[1] * ss));
+    const int sh = static_cast<int>(roundf(roi[2] * ss));
+    const int ew = static_cast<int>(roundf(roi[3] * ss));
+    const int eh = static_cast<int>(roundf(roi[4] * ss));
+    if (b < 0 || b >= N) return 1;
+    const int rw = max(ew - sw + 1, 1), rh = max(eh - sh + 1, 1);
+    const int hv = min(sh + rh + 1, H) - max(sh, 0);
+    const int wv = min(sw + rw + 1, W) - max(sw, 0);
+    if (hv <= 0 || wv <= 0) return 1;
+    const int mh = min(static_cast<int>(static_cast<float>(rh) * __frcp_rn(static_cast<float>(PH))) + 2, hv);
+    const int mw = min(static_cast<int>(static_cast<float>(rw) * __frcp_rn(static_cast<float>(PW))) + 2, wv);
+    return mh * mw + 6;
+}
+
+template <int NT>
+__device__ __forceinline__ int block_min(int v, int64_t* red) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    int m = v;
+    for (int w = 0; w < NT / 64; ++w) m = min(m, static_cast<int>(red[w]));
+    return m;
+}
+
+// Cost-balanced forward for RoIs grouped by batch index (proposals;
+// train.py's sample_rois), two launches:
+//
+// roi_partition_kernel (one workgroup): per-RoI cost (roi_cost_fast), prefix
+// sum, and a cut of the RoI list into S contiguous segments of equal cost
+// (RoI t goes to the 1/S slice holding its cost midpoint): seg_lo[0..S],
+// plus, per segment, the positions where the batch index changes (up to
+// kBalMaxRuns - 1 listed; the count is exact).
+//
+// roi_pool_fwd_bal_kernel, grid (S, C/8): workgroup (s, g) produces channels
+// [8g, 8g+8) of segment s -- every workgroup of the (one resident round) grid
+// gets the same work, so they end together; a split by RoI count waits for
+// the workgroup that drew the largest RoIs.  It walks its segment in runs of
+// equal batch index (usually one or two), stages that image's 8-channel tile
+// into LDS as pixel-major [H*W][8], and its waves pull RoIs from an LDS
+// counter: lane = bin, each lane scans its bin window once, 8 channel maxima
+// from two ds_read_b128 per pixel, strict '>' in row-major order (the CPU
+// kernel's first-max rule).  Runs split at every batch index change, so the
+// result is exact for any RoI order (only slower when RoIs are not grouped).
+constexpr int kBalMaxRuns = 32;
+constexpr int kSegInfo = 1 + kBalMaxRuns;  // per segment: #changes, change positions
+// tools-only timeline probe (variant "baldbg"): per workgroup, s_memrealtime
+// (100 MHz) at entry / after the partition / after the first tile / exit
+__device__ unsigned long long g_bal_dbg[8 * 8192];
+
+template <int NT, int COST>
+__global__ __launch_bounds__(NT) void roi_partition_kernel(const float* __restrict__ rois, int R, int N,
+                                                           int H, int W, int PH, int PW, float ss, int S,
+                                                           int* __restrict__ seg_lo,
+                                                           int* __restrict__ seg_info) {
+    constexpr int NWV = NT / 64;
+    __shared__ int64_t s_red[NWV];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (int q = tid; q < S; q += NT) seg_info[static_cast<size_t>(q) * kSegInfo] = 0;
+    const int per_w = (R + NWV - 1) / NWV;
+    const int wt0 = min(wid * per_w, R), wt1 = min(wt0 + per_w, R);
+    auto cost = [&](int t) { return COST ? roi_cost_fast(rois, t, ss, N, H, W, PH, PW) : 1; };
+    int64_t wsum = 0;
+    for (int t = wt0 + lane; t < wt1; t += 64) wsum += cost(t);
+    for (int o = 32; o > 0; o >>= 1) wsum += __shfl_xor(wsum, o, 64);
+    if (lane == 0) s_red[wid] = wsum;
+    __syncthreads();  // also orders the counter zeroing before the atomics below
+    int64_t carry = 0, total = 0;
+    for (int w = 0; w < NWV; ++w) {
+        carry += w < wid ? s_red[w] : 0;
+        total += s_red[w];
+    }
+    const double scale = static_cast<double>(S) / (2.0 * static_cast<double>(total));
+    auto seg_at = [&](int64_t pre, int c) {
+        const int st = static_cast<int>(static_cast<double>(2 * pre + c) * scale);
+        return st < S - 1 ? st : S - 1;
+    };
+    // (segment, batch index) of the RoI before the current one
+    int prev_seg = -1, prev_b = 0;
+    if (wt0 > 0 && wt0 < wt1) {
+        const int cp = cost(wt0 - 1);
+        prev_seg = seg_at(carry - cp, cp);
+        prev_b = static_cast<int>(rois[static_cast<size_t>(wt0 - 1) * 5]);
+    }
+    for (int base = wt0; base < wt1; base += 64) {
+        const int t = base + lane;
+        const bool in = t < wt1;
+        const int c = in ? cost(t) : 0;
+        const int bt = in ? static_cast<int>(rois[static_cast<size_t>(t) * 5]) : 0;
+        int64_t inc = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        const int st = in ? seg_at(carry + inc - c, c) : S;
+        int ps = __shfl_up(st, 1, 64), pb = __shfl_up(bt, 1, 64);
+        if (lane == 0) {
+            ps = prev_seg;
+            pb = prev_b;
+        }
+        if (in) {
+            for (int q = ps + 1; q <= st; ++q) seg_lo[q] = t;  // first RoI of segments (ps, st]
+            if (t > 0 && st == ps && bt != pb) {               // batch change inside a segment
+                const int k = atomicAdd(&seg_info[static_cast<size_t>(st) * kSegInfo], 1);
+                if (k < kBalMaxRuns - 1) seg_info[static_cast<size_t>(st) * kSegInfo + 1 + k] = t;
+            }
+        }
+        const int last = min(63, wt1 - 1 - base);  // last lane holding a RoI
+        carry += __shfl(inc, last, 64);
+        prev_seg = __shfl(st, last, 64);
+        prev_b = __shfl(bt, last, 64);
+    }
+    // segments after the last RoI's are empty: the wave holding RoI R-1 closes them
+    if (wt0 < wt1 && wt1 == R)
+        for (int q = prev_seg + 1 + lane; q <= S; q += 64) seg_lo[q] = R;
+}
+
+// MODE (tools/ab_roi_pool.py diagnostics only): 0 = the op; 1 = no pooling
+// (stores 0 / -1: staging + store floor); 2 = pooling, stores only if an
+// impossible value shows up (compute floor)
+template <int NT, bool DBG = false, int MODE = 0>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void roi_pool_fwd_bal_kernel(
+    const float* __restrict__ x, const float* __restrict__ rois, const int* __restrict__ seg_lo,
+    const int* __restrict__ seg_info, int N, int C, int H, int W, int PH, int PW, float ss,
+    float* __restrict__ out, int32_t* __restrict__ argmax) {
+    constexpr int CG = 8;
+    extern __shared__ __attribute__((aligned(16))) float4 tile4[];  // [H*W][2] float4
+    __shared__ int64_t s_red[NT / 64];
+    __shared__ int s_runs[kBalMaxRuns];
+    __shared__ int s_next;
+    const int seg = blockIdx.x;
+    const int c0 = blockIdx.y * CG;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int HW = H * W;
+    const int PHW = PH * PW;
+    const unsigned wg = blockIdx.x + blockIdx.y * gridDim.x;
+    if (DBG && tid == 0 && wg < 8192) {
+        g_bal_dbg[wg * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+        unsigned hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        g_bal_dbg[wg * 8 + 5] = hw;
+    }
+    const int lo = seg_lo[seg], hi = seg_lo[seg + 1];
+    const int* info = seg_info + static_cast<size_t>(seg) * kSegInfo;
+    const int n_chg = info[0];
+    const int n_runs = hi > lo ? n_chg + 1 : 0;
+    const bool listed = n_runs <= kBalMaxRuns;
+    if (listed && wid == 0 && n_runs > 1) {  // run starts: lo, then the sorted change positions
+        int v = lane < n_chg ? info[1 + lane] : 0x7fffffff;
+        for (int k = 2; k <= 64; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                const int o = __shfl_xor(v, j, 64);
+                const bool up = (lane & k) == 0, low = (lane & j) == 0;
+                v = (low == up) ? min(v, o) : max(v, o);
+            }
+        if (lane < n_chg) s_runs[1 + lane] = v;
+    }
+    if (tid == 0) s_runs[0] = lo;
+    __syncthreads();
+    if (DBG && tid == 0 && wg < 8192) {
+        g_bal_dbg[wg * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+        g_bal_dbg[wg * 8 + 6] = (static_cast<unsigned long long>(hi - lo) << 32) | n_runs;
+    }
+    // 3. per run: stage the tile, pool every RoI of the run
+    const int ph = lane / PW, pw = lane - (lane / PW) * PW;
+    const bool act = lane < PHW;
+    int run = 0;
+    int t_run = lo;
+    while (t_run < hi) {
+        const int b = static_cast<int>(rois[static_cast<size_t>(t_run) * 5]);
+        int t_end;
+        if (listed) {
+            t_end = run + 1 < n_runs ? s_runs[run + 1] : hi;
+            ++run;
+        } else {
+            int first = hi;
+            for (int t = t_run + 1 + tid; t < hi; t += NT)
+                if (static_cast<int>(rois[static_cast<size_t>(t) * 5]) != b) {
+                    first = t;
+                    break;
+                }
+            t_end = block_min<NT>(first, s_red);
+        }
+        const bool valid = b >= 0 && b < N;
+        __syncthreads();  // the previous run's waves are done with the tile and s_next
+        if (valid) {
+            const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+            for (int p = tid; p < HW; p += NT) {
+                float v[CG];
+#pragma unroll
+                for (int q = 0; q < CG; ++q) v[q] = src[static_cast<size_t>(q) * HW + p];
+                tile4[2 * p] = make_float4(v[0], v[1], v[2], v[3]);
+                tile4[2 * p + 1] = make_float4(v[4], v[5], v[6], v[7]);
+            }
+        }
+        if (tid == 0) s_next = t_run;
+        __syncthreads();
+        if (DBG && tid == 0 && wg < 8192 && run <= 1) g_bal_dbg[wg * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+        int t = 0;
+        if (lane == 0) t = atomicAdd(&s_next, 1);
+        t = __builtin_amdgcn_readfirstlane(t);
+        while (t < t_end) {
+            int tn = 0;
+            if (lane == 0) tn = atomicAdd(&s_next, 1);  // prefetch the next item
+            const size_t o = (static_cast<size_t>(t) * C + c0) * PHW + lane;
+            float mv[CG];
+            int mi[CG];
+            if (valid && MODE != 1) {
+                const RoiGeom gm = roi_geom(rois + static_cast<size_t>(t) * 5, ss, PH, PW);
+                int4 g = geom_bin(gm, H, W, ph, pw);
+                if (!act) g = make_int4(0, 0, 0, 0);
+                const bool empty = g.y <= g.x || g.w <= g.z;
+#pragma unroll
+                for (int c = 0; c < CG; ++c) {
+                    mv[c] = empty ? 0.0f : -FLT_MAX;
+                    mi[c] = -1;
+                }
+                for (int h = g.x; h < g.y; ++h) {
+                    int ii = h * W + g.z;
+                    const int iend = h * W + g.w;
+                    for (; ii < iend; ++ii) {
+                        const float4 lo4 = tile4[2 * ii];
+                        const float4 hi4 = tile4[2 * ii + 1];
+                        const float v[CG] = {lo4.x, lo4.y, lo4.z, lo4.w, hi4.x, hi4.y, hi4.z, hi4.w};
+#pragma unroll
+                        for (int c = 0; c < CG; ++c) {
+                            if (v[c] > mv[c]) {
+                                mv[c] = v[c];
+                                mi[c] = ii;
+                            }
+                        }
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < CG; ++c) {
+                    mv[c] = 0.0f;
+                    mi[c] = -1;
+                }
+            }
+            if (act && (MODE != 2 || mv[0] == 1234.5f)) {
+#pragma unroll
+                for (int c = 0; c < CG; ++c) {
+                    out[o + static_cast<size_t>(c) * PHW] = mv[c];
+                    argmax[o + static_cast<size_t>(c) * PHW] = mi[c];
+                }
+            }
+            t = __builtin_amdgcn_readfirstlane(tn);
+        }
+        t_run = t_end;
+    }
+    if (DBG) {
+        __syncthreads();
+        if (tid == 0 && wg < 8192) g_bal_dbg[wg * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+// ------------------------------------------------ balanced forward, v2
+// Same partition, runs and tile as roi_pool_fwd_bal_kernel; the per-RoI loop
+// is wave-uniform: every lane walks the wave's largest bin window, (max bin
+// height) x (max bin width), row-major over its own window with the row /
+// column clamped to its last one.  A clamped step revisits a pixel the lane
+// has already seen, which can never pass the strict '>' again, so each lane's
+// (max, first index) is exactly its own row-major scan's; an empty bin reads
+// the -inf pad pixel (index H*W).  Loop control is scalar (no exec-mask
+// updates per pixel) and two pixels are in flight per step.
+// SWAP: half the lanes of every ds_read_b128 lane group read a pixel's two
+// 16-B slots in the other order, so lanes on pixels 8k apart hit different
+// slots; such a lane's registers 0-3 hold channels 4-7 (a fixed per-lane
+// permutation, undone by its store addresses).
+// FIX: PH = PW = FIX at compile time (the reference's 7x7, nets/heads.py:8):
+// constant lane -> bin map and immediate store offsets.
+// XCD-aware order: workgroups go round-robin over the 8 XCDs by linear id
+// (= blockIdx.x mod 8 when S % 8 == 0); each XCD gets a contiguous run of
+// S/8 segments, so the workgroups staging the same image tile share an L2.
+// MODE (diagnostics, tools/ab_roi_pool.py): 0 = the op; 2 = no stores;
+// 3 = no stores and every lane reads lane 0's pixel (no bank conflicts).
+__device__ __forceinline__ int wave_max_i32(int v) {
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
+// Strict '>' update of 8 running (max, first index) pairs with one pixel.
+__device__ __forceinline__ void take8(const float4& a, const float4& b, int ii, float (&mv)[8],
+                                      int (&mi)[8]) {
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        if (v[c] > mv[c]) {
+            mv[c] = v[c];
+            mi[c] = ii;
+        }
+    }
+}
+
+template <int NT, int FIX, bool SWAP, int MODE>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void roi_pool_fwd_bal2_kernel(
+    const float* __restrict__ x, const float* __restrict__ rois, const int* __restrict__ seg_lo,
+    const int* __restrict__ seg_info, int N, int C, int H, int W, int PH_, int PW_, float ss,
+    float* __restrict__ out, int32_t* __restrict__ argmax) {
+    constexpr int CG = 8;
+    extern __shared__ __attribute__((aligned(16))) float4 tile4[];  // [H*W + 1][2] float4
+    __shared__ int64_t s_red[NT / 64];
+    __shared__ int s_runs[kBalMaxRuns];
+    __shared__ int s_next;
+    const int PH = FIX ? FIX : PH_, PW = FIX ? FIX : PW_;
+    const int S = gridDim.x;
+    const int seg = (S % 8 == 0) ? static_cast<int>(blockIdx.x % 8) * (S / 8) + static_cast<int>(blockIdx.x / 8)
+                                 : static_cast<int>(blockIdx.x);
+    const int c0 = blockIdx.y * CG;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int HW = H * W;
+    const int PHW = PH * PW;
+    if (tid < 2) tile4[2 * HW + tid] = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    const int lo = seg_lo[seg], hi = seg_lo[seg + 1];
+    const int* info = seg_info + static_cast<size_t>(seg) * kSegInfo;
+    const int n_chg = info[0];
+    const int n_runs = hi > lo ? n_chg + 1 : 0;
+    const bool listed = n_runs <= kBalMaxRuns;
+    if (listed && wid == 0 && n_runs > 1) {  // run starts: lo, then the sorted change positions
+        int v = lane < n_chg ? info[1 + lane] : 0x7fffffff;
+        for (int k = 2; k <= 64; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                const int o = __shfl_xor(v, j, 64);
+                const bool up = (lane & k) == 0, low = (lane & j) == 0;
+                v = (low == up) ? min(v, o) : max(v, o);
+            }
+        if (lane < n_chg) s_runs[1 + lane] = v;
+    }
+    if (tid == 0) s_runs[0] = lo;
+    __syncthreads();
+    const int ph = lane / PW, pw = lane - (lane / PW) * PW;
+    const bool act = lane < PHW;
+    const int swp = SWAP ? ((lane >> 2) & 1) : 0;
+    const char* tb = reinterpret_cast<const char*>(tile4);
+    const int offa = swp * 16;
+    int run = 0;
+    int t_run = lo;
+    while (t_run < hi) {
+        const int b = static_cast<int>(rois[static_cast<size_t>(t_run) * 5]);
+        int t_end;
+        if (listed) {
+            t_end = run + 1 < n_runs ? s_runs[run + 1] : hi;
+            ++run;
+        } else {
+            int first = hi;
+            for (int t = t_run + 1 + tid; t < hi; t += NT)
+                if (static_cast<int>(rois[static_cast<size_t>(t) * 5]) != b) {
+                    first = t;
+                    break;
+                }
+            t_end = block_min<NT>(first, s_red);
+        }
+        const bool valid = b >= 0 && b < N;
+        __syncthreads();  // the previous run's waves are done with the tile and s_next
+        if (valid) {
+            const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+            for (int p = tid; p < HW; p += NT) {
+                float v[CG];
+#pragma unroll
+                for (int q = 0; q < CG; ++q) v[q] = src[static_cast<size_t>(q) * HW + p];
+                tile4[2 * p] = make_float4(v[0], v[1], v[2], v[3]);
+                tile4[2 * p + 1] = make_float4(v[4], v[5], v[6], v[7]);
+            }
+        }
+        if (tid == 0) s_next = t_run;
+        __syncthreads();
+        int t = 0;
+        if (lane == 0) t = atomicAdd(&s_next, 1);
+        t = __builtin_amdgcn_readfirstlane(t);
+        while (t < t_end) {
+            int tn = 0;
+            if (lane == 0) tn = atomicAdd(&s_next, 1);  // prefetch the next item
+            float mv[CG];
+            int mi[CG];
+            if (valid) {
+                const RoiGeom gm = roi_geom(rois + static_cast<size_t>(t) * 5, ss, PH, PW);
+                const int4 g = geom_bin(gm, H, W, ph, pw);
+                const int hgt = g.y - g.x, wdt = g.w - g.z;
+                const bool empty = hgt <= 0 || wdt <= 0;
+                const bool live = act && !empty;
+#pragma unroll
+                for (int c = 0; c < CG; ++c) {
+                    mv[c] = empty ? 0.0f : -FLT_MAX;
+                    mi[c] = -1;
+                }
+                const int MH = wave_max_i32(live ? hgt : 0);
+                const int MW = wave_max_i32(live ? wdt : 0);
+                const int lastr = live ? hgt - 1 : 0, lastc = live ? wdt - 1 : 0;
+                const int org = live ? g.x * W + g.z : HW;  // window origin; dead lanes: pad pixel
+                const int rstep = live ? W : 0;
+                const int tot = MH * MW;
+                int dh = 0, dw = 0, rowi = org;
+                for (int s = 0; s < tot; s += 2) {
+                    if (dw == 0) rowi = org + min(dh, lastr) * rstep;
+                    const int iiA = rowi + min(dw, lastc);
+                    if (++dw == MW) {
+                        dw = 0;
+                        ++dh;
+                    }
+                    int iiB = iiA;  // past the end: a revisit of A
+                    if (s + 1 < tot) {
+                        if (dw == 0) rowi = org + min(dh, lastr) * rstep;
+                        iiB = rowi + min(dw, lastc);
+                        if (++dw == MW) {
+                            dw = 0;
+                            ++dh;
+                        }
+                    }
+                    const int rA = MODE == 3 ? __builtin_amdgcn_readfirstlane(iiA) : iiA;
+                    const int rB = MODE == 3 ? __builtin_amdgcn_readfirstlane(iiB) : iiB;
+                    const int adA = rA * 32 + offa, adB = rB * 32 + offa;
+                    const float4 a0 = *reinterpret_cast<const float4*>(tb + adA);
+                    const float4 a1 = *reinterpret_cast<const float4*>(tb + (adA ^ 16));
+                    const float4 b0 = *reinterpret_cast<const float4*>(tb + adB);
+                    const float4 b1 = *reinterpret_cast<const float4*>(tb + (adB ^ 16));
+                    take8(a0, a1, iiA, mv, mi);
+                    take8(b0, b1, iiB, mv, mi);
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < CG; ++c) {
+                    mv[c] = 0.0f;
+                    mi[c] = -1;
+                }
+            }
+            if (act && (MODE == 0 || mv[0] == 1234.5f)) {
+                // registers 0-3 / 4-7 hold channels 0-3 / 4-7, swapped when swp
+                const size_t o = (static_cast<size_t>(t) * C + c0) * PHW + lane;
+                const size_t qa = static_cast<size_t>(swp) * 4 * PHW;
+                const size_t qb = static_cast<size_t>(4 - 4 * swp) * PHW;
+                float* oa = out + o + qa;
+                float* ob = out + o + qb;
+                int32_t* ia = argmax + o + qa;
+                int32_t* ib = argmax + o + qb;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    oa[c * PHW] = mv[c];
+                    ob[c * PHW] = mv[4 + c];
+                    ia[c * PHW] = mi[c];
+                    ib[c * PHW] = mi[4 + c];
+                }
+            }
+            t = __builtin_amdgcn_readfirstlane(tn);
+        }
+        t_run = t_end;
+    }
+}
+
 // Flattened, software-pipelined pixel-major variant.  The LDS tile is
 // [H*W+1][CG] (CG = 4 or 8 channels per pixel, one or two ds_read_b128); a lane
 // walks its bin window as ONE loop over bin_h*bin_w pixels (row-major, so the
@@ -870,11 +1330,46 @@ FwdWs carve_fwd(void* ws, int64_t R, int N, int C) {
 }
 constexpr int kFwdCG = 4;                       // channels per image tile
 constexpr size_t kFwdTileBudget = 96 * 1024;    // LDS for the CG planes
+constexpr size_t kLdsPerCu = 160 * 1024;        // gfx950
+constexpr size_t kBalStatic = 1024;             // static LDS of the balanced kernel (rounded up)
+// default forward for image-grouped RoIs: 0 = px8 (count split), 2 = balanced v2
+constexpr int kSortedDefault = 0;
+
+int device_cu_count();
+// segments of the balanced forward: at most two resident workgroups per CU
+int bal_max_segments() { return 2 * device_cu_count(); }
+struct BalWs {
+    int* seg_lo;
+    int* seg_info;
+    size_t bytes;
+};
+BalWs carve_bal(void* ws, int S) {
+    Carver c(ws);
+    BalWs w{};
+    w.seg_lo = c.take<int>(static_cast<size_t>(S) + 1);
+    w.seg_info = c.take<int>(static_cast<size_t>(S) * kSegInfo);
+    w.bytes = c.used();
+    return w;
+}
+int device_cu_count() {
+    static int cus = 0;
+    if (cus <= 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+            cus = n;
+        else
+            cus = 256;
+    }
+    return cus;
+}
 }  // namespace
 
 extern "C" size_t frcnn_roi_pool_fwd_workspace_size(int64_t R, int N, int C) {
     if (R < 0 || N < 0 || C < 0) return 0;
-    return carve_fwd(nullptr, R, N, C).bytes;
+    const size_t a = carve_fwd(nullptr, R, N, C).bytes;
+    const size_t b = carve_bal(nullptr, bal_max_segments()).bytes;
+    return a > b ? a : b;
 }
 
 extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, int N, int C,
@@ -893,13 +1388,87 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
     const bool aligned = (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
                          (reinterpret_cast<uintptr_t>(argmax) % 16 == 0);
     const char* var = getenv("FRCNN_ROIPOOL_VARIANT");  // A/B override (tests, tools/ab_roi_pool.py)
+    auto is = [&](const char* v) { return var && std::strcmp(var, v) == 0; };
     const bool px8_ok = N > 0 && HW > 0 && C % 8 == 0 && 2 * tile_bytes <= kFwdTileBudget &&
                         PH * PW <= 64;
     const int64_t per_img = (R + (N > 0 ? N : 1) - 1) / (N > 0 ? N : 1);
     int64_t split8 = px8_ok ? (512 + static_cast<int64_t>(C / 8) * N - 1) / (static_cast<int64_t>(C / 8) * N) : 1;
     split8 = split8 < 1 ? 1 : (split8 > 64 ? 64 : split8);
-    // default: one launch (px8, 16-wave workgroups) when the RoIs are grouped by image
-    if (px8_ok && rois_sorted && !var) {
+    // default for RoIs grouped by image: one launch, cost-balanced over a
+    // grid of exactly one resident round (2 x 1024-thread workgroups per CU
+    // when two 8-channel tiles fit the CU's LDS)
+    const size_t bal_lds = 2 * tile_bytes;
+    const bool bal_ok = N > 0 && HW > 0 && C % 8 == 0 && PH * PW <= 64 &&
+                        bal_lds + kBalStatic <= kLdsPerCu && R < (1 << 21) && C / 8 <= 65535;
+    const bool bal2_var = is("bal2") || is("bal2ns") || is("bal2c") || is("bal2b");
+    if (bal_ok && rois_sorted && (bal2_var || (kSortedDefault == 2 && !var))) {
+        const int groups = C / 8;
+        const size_t lds2 = bal_lds + 32;  // + the -inf pad pixel
+        const int per_cu = kLdsPerCu / (lds2 + kBalStatic) >= 2 ? 2 : 1;
+        int64_t S = static_cast<int64_t>(device_cu_count()) * per_cu / groups;
+        S = S < 1 ? 1 : S;
+        S = S > R ? R : S;
+        S = S > bal_max_segments() ? bal_max_segments() : S;
+        BalWs w = carve_bal(workspace, static_cast<int>(S));
+        FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_fwd: workspace %zu < %zu",
+                      ws_bytes, w.bytes);
+        hipLaunchKernelGGL((roi_partition_kernel<1024, 1>), dim3(1), dim3(1024), 0, st, rois,
+                           static_cast<int>(R), N, H, W, PH, PW, spatial_scale, static_cast<int>(S),
+                           w.seg_lo, w.seg_info);
+        FRCNN_LAUNCH_CHECK("roi_partition_kernel");
+        const dim3 grid(static_cast<unsigned>(S), groups);
+        const bool fix7 = PH == 7 && PW == 7;
+#define FRCNN_BAL2(FX, SW, MD)                                                                         \
+    hipLaunchKernelGGL((roi_pool_fwd_bal2_kernel<1024, FX, SW, MD>), grid, dim3(1024), lds2, st, x, rois, \
+                       w.seg_lo, w.seg_info, N, C, H, W, PH, PW, spatial_scale, out, argmax)
+        if (is("bal2ns")) {
+            if (fix7) FRCNN_BAL2(7, false, 0); else FRCNN_BAL2(0, false, 0);
+        } else if (is("bal2c")) {
+            if (fix7) FRCNN_BAL2(7, true, 2); else FRCNN_BAL2(0, true, 2);
+        } else if (is("bal2b")) {
+            if (fix7) FRCNN_BAL2(7, true, 3); else FRCNN_BAL2(0, true, 3);
+        } else {
+            if (fix7) FRCNN_BAL2(7, true, 0); else FRCNN_BAL2(0, true, 0);
+        }
+#undef FRCNN_BAL2
+        FRCNN_LAUNCH_CHECK("roi_pool_fwd_bal2_kernel");
+        return FRCNN_OK;
+    }
+    if (bal_ok && rois_sorted && (is("bal") || is("balcnt") || is("baldbg") || is("balnc") || is("balns"))) {
+        const int groups = C / 8;
+        const int per_cu = kLdsPerCu / (bal_lds + kBalStatic) >= 2 ? 2 : 1;
+        int64_t S = static_cast<int64_t>(device_cu_count()) * per_cu / groups;
+        S = S < 1 ? 1 : S;
+        S = S > R ? R : S;
+        S = S > bal_max_segments() ? bal_max_segments() : S;
+        BalWs w = carve_bal(workspace, static_cast<int>(S));
+        FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_fwd: workspace %zu < %zu",
+                      ws_bytes, w.bytes);
+        if (is("balcnt"))
+            hipLaunchKernelGGL((roi_partition_kernel<1024, 0>), dim3(1), dim3(1024), 0, st, rois,
+                               static_cast<int>(R), N, H, W, PH, PW, spatial_scale, static_cast<int>(S),
+                               w.seg_lo, w.seg_info);
+        else
+            hipLaunchKernelGGL((roi_partition_kernel<1024, 1>), dim3(1), dim3(1024), 0, st, rois,
+                               static_cast<int>(R), N, H, W, PH, PW, spatial_scale, static_cast<int>(S),
+                               w.seg_lo, w.seg_info);
+        FRCNN_LAUNCH_CHECK("roi_partition_kernel");
+        if (is("balnc") || is("balns"))
+            hipLaunchKernelGGL((is("balnc") ? roi_pool_fwd_bal_kernel<1024, false, 1> : roi_pool_fwd_bal_kernel<1024, false, 2>),
+                               dim3(static_cast<unsigned>(S), groups), dim3(1024), bal_lds, st, x, rois, w.seg_lo,
+                               w.seg_info, N, C, H, W, PH, PW, spatial_scale, out, argmax);
+        else if (is("baldbg"))
+            hipLaunchKernelGGL((roi_pool_fwd_bal_kernel<1024, true>), dim3(static_cast<unsigned>(S), groups),
+                               dim3(1024), bal_lds, st, x, rois, w.seg_lo, w.seg_info, N, C, H, W, PH, PW,
+                               spatial_scale, out, argmax);
+        else
+            hipLaunchKernelGGL((roi_pool_fwd_bal_kernel<1024, false>), dim3(static_cast<unsigned>(S), groups),
+                               dim3(1024), bal_lds, st, x, rois, w.seg_lo, w.seg_info, N, C, H, W, PH, PW,
+                               spatial_scale, out, argmax);
+        FRCNN_LAUNCH_CHECK("roi_pool_fwd_bal_kernel");
+        return FRCNN_OK;
+    }
+    if (px8_ok && rois_sorted && (is("px8sorted") || (kSortedDefault == 0 && !var))) {
         dim3 grid(C / 8, N + 1, static_cast<unsigned>(split8));
         hipLaunchKernelGGL((roi_pool_fwd_px8_kernel<1024, true>), grid, dim3(1024), 2 * tile_bytes, st,
                            x, rois, nullptr, nullptr, nullptr, static_cast<int>(R), C, H, W, PH, PW,
@@ -920,7 +1489,6 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
         split = split < cap ? split : cap;
         split = split < 1 ? 1 : (split > 64 ? 64 : split);
         const size_t pad = 8 * sizeof(float);
-        auto is = [&](const char* v) { return var && std::strcmp(var, v) == 0; };
         if (px8_ok && !(var && var[0] == 'w') && !is("tile") && !is("px8s") && !is("pxf8") &&
             !is("pxf4") && !is("px8")) {
             dim3 grid(C / 8, N, static_cast<unsigned>(split8));  // default (unsorted RoIs)
@@ -1049,4 +1617,10 @@ extern "C" int frcnn_roi_pool_bwd(const float* grad, const float* rois, const in
     }
     FRCNN_LAUNCH_CHECK("roi_pool_bwd_kernel");
     return FRCNN_OK;
+}
+
+// tools-only (not part of the C-ABI): copy the "baldbg" timeline probe to host
+extern "C" int frcnn_dbg_bal_stamps(unsigned long long* host, int n) {
+    if (n > 8 * 8192) n = 8 * 8192;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bal_dbg), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -2;
 }

@@ -55,12 +55,10 @@ def _roi_pool_fwd(x: torch.Tensor, rois: torch.Tensor, ph: int, pw: int, ss: flo
     R = rois.size(0)
     out = torch.empty((R, C, ph, pw), dtype=torch.float32, device=x.device)
     am = torch.empty((R, C, ph, pw), dtype=torch.int32, device=x.device)
-    ws = None if rois_sorted else _lib.workspace(lib.frcnn_roi_pool_fwd_workspace_size(R, N, C),
-                                                 x.device)
+    ws = _lib.workspace(lib.frcnn_roi_pool_fwd_workspace_size(R, N, C), x.device)
     _lib.check(lib.frcnn_roi_pool_fwd(_lib.ptr(x), _lib.ptr(rois), R, N, C, H, W, ph, pw, float(ss),
                                       int(bool(rois_sorted)), _lib.ptr(out), _lib.ptr(am),
-                                      _lib.ptr(ws), 0 if ws is None else ws.numel(),
-                                      _lib.stream_ptr()), "roi_pool forward")
+                                      _lib.ptr(ws), ws.numel(), _lib.stream_ptr()), "roi_pool forward")
     return out, am
 
 

@@ -213,7 +213,7 @@ def test_propose_edge_cases(case, path):
     fh, fw, img_h, img_w = 20, 30, 320, 480
     anchors = orc.generate_anchors(orc.generate_anchor_base(), 16, fw, fh)
     n = len(anchors)
-    r = np.random.default_rng(hash(case) % 1000)
+    r = np.random.default_rng(sum(map(ord, case)))
     sc = synth.rpn_scores(n, 9, 0)
     de = synth.rpn_deltas(n, 9, 0)
     pre, post, thr = 3000, 300, 0.7
@@ -267,8 +267,8 @@ def test_roi_pool_special_values(variant, monkeypatch):
     assert np.array_equal(out.cpu().numpy().view(np.uint32), oo.view(np.uint32))
 
 
-@pytest.mark.parametrize("variant", ["sorted", "px8w16", "px8s", "px8", "pxf8", "pxf4", "wave8",
-                                     "wave4", "tile"])
+@pytest.mark.parametrize("variant", ["sorted", "px8sorted", "px8w16", "px8s", "px8", "pxf8", "pxf4",
+                                     "wave8", "wave4", "tile"])
 def test_roi_pool_variants_random(variant, monkeypatch):
     """Every forward variant, cfg2-like random RoIs, bit-exact vs the oracle
     ("sorted" = the default single-launch path for RoIs grouped by image)."""
@@ -285,7 +285,106 @@ def test_roi_pool_variants_random(variant, monkeypatch):
     wh = r.uniform(0, 40, (R, 2)).astype(np.float32)
     rois = np.concatenate([b[:, None], xy, xy + wh], 1).astype(np.float32)
     out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7,
-                                       rois_sorted=(variant == "sorted"))
+                                       rois_sorted=variant in ("sorted", "px8sorted"))
     oo, oa = orc.roi_pool_forward(x, rois, 7)
     assert np.array_equal(am.cpu().numpy(), oa)
     assert np.array_equal(out.cpu().numpy(), oo)
+
+
+def _rand_rois(r, b, H, W, lo=-3, span=40):
+    xy = r.uniform(lo, max(H, W) + 2, (len(b), 2)).astype(np.float32)
+    wh = r.uniform(0, span, (len(b), 2)).astype(np.float32)
+    return np.concatenate([np.asarray(b, np.float32)[:, None], xy, xy + wh], 1).astype(np.float32)
+
+
+@pytest.mark.parametrize("variant", ["bal2", "bal"])
+@pytest.mark.parametrize("case", ["many_images", "invalid_ends", "unsorted_promised_sorted",
+                                  "single_roi", "gaps", "one_image_tiny_rois", "uniform_sizes",
+                                  "ph5", "cfg4_shape"])
+def test_roi_pool_balanced_path(case, variant, monkeypatch):
+    """The cost-balanced single-launch forward (default for RoIs grouped by
+    image): segment boundaries, run lists (and their overflow / block-search
+    fallback), out-of-range batch indices, and any RoI order bit-exact."""
+    monkeypatch.setenv("FRCNN_ROIPOOL_VARIANT", variant)
+    r = np.random.default_rng(sum(map(ord, case)))
+    ph = 5 if case == "ph5" else 7
+    N, C, H, W = 4, 16, 20, 27
+    span = 40
+    if case == "many_images":  # > 32 runs per segment and > 2 run starts per thread chunk
+        N, C, H, W, span = 20000, 8, 4, 5, 6
+        b = np.sort(r.integers(0, N, 40000))
+    elif case == "invalid_ends":
+        b = np.concatenate([[-1, -1], np.sort(r.integers(0, N, 200)), [N, N, N + 3]])
+    elif case == "unsorted_promised_sorted":
+        b = r.integers(0, N, 500)
+    elif case == "single_roi":
+        b = np.array([2])
+    elif case == "gaps":  # images 1 and 2 have no RoIs
+        b = np.sort(np.concatenate([np.zeros(60, int), np.full(90, 3)]))
+    elif case == "cfg4_shape":  # 50x84 tile: one workgroup per CU
+        N, C, H, W = 1, 16, 50, 84
+        b = np.zeros(500, int)
+    elif case == "one_image_tiny_rois":
+        N, b, span = 1, np.zeros(3000, int), 2
+    else:
+        b = np.sort(r.integers(0, N, 700))
+    x = r.standard_normal((N, C, H, W), dtype=np.float32)
+    x[:, :, 2:9, 3:12] = np.round(x[:, :, 2:9, 3:12])  # ties
+    rois = _rand_rois(r, b, H, W, span=span)
+    if case == "uniform_sizes":
+        rois[:, 3:] = rois[:, 1:3] + 6.0
+    out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), ph,
+                                       rois_sorted=True)
+    oo, oa = orc.roi_pool_forward(x, rois, ph)
+    valid = (b >= 0) & (b < N)
+    assert np.array_equal(am.cpu().numpy()[valid], oa[valid])
+    assert np.array_equal(out.cpu().numpy()[valid].view(np.uint32), oo[valid].view(np.uint32))
+    assert (out.cpu().numpy()[~valid] == 0).all() and (am.cpu().numpy()[~valid] == -1).all()
+
+
+@pytest.mark.parametrize("variant", ["bal2", "bal2ns", "bal", "px8sorted"])
+def test_roi_pool_sorted_variants_cfg2(variant, monkeypatch):
+    """The two single-launch forwards for image-grouped RoIs at the bench shape
+    (8 x 256 x 38 x 63, 300 proposals per image) agree bit for bit with the
+    oracle on a sample of images."""
+    monkeypatch.setenv("FRCNN_ROIPOOL_VARIANT", variant)
+    r = np.random.default_rng(5)
+    N, C, H, W, per = 8, 256, 38, 63, 300
+    x = r.standard_normal((N, C, H, W), dtype=np.float32)
+    b = np.repeat(np.arange(N), per)
+    rois = _rand_rois(r, b, H, W, span=45)
+    out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7,
+                                       rois_sorted=True)
+    pick = np.concatenate([np.arange(0, 40), np.arange(1190, 1230), np.arange(2360, 2400)])
+    oo, oa = orc.roi_pool_forward(x, rois[pick], 7)
+    assert np.array_equal(am.cpu().numpy()[pick], oa)
+    assert np.array_equal(out.cpu().numpy()[pick], oo)
+
+
+@pytest.mark.parametrize("variant", ["bal2", "bal2ns", "bal", "px8sorted"])
+def test_roi_pool_sorted_special_values(variant, monkeypatch):
+    """The image-grouped forwards on signed zeros, -FLT_MAX, +-inf and NaN
+    windows, RoIs partly / fully outside the map (bal2: clamped revisits and
+    the -inf pad pixel) -- bit-exact vs the oracle."""
+    monkeypatch.setenv("FRCNN_ROIPOOL_VARIANT", variant)
+    r = np.random.default_rng(7)
+    N, C, H, W = 2, 16, 12, 14
+    x = r.standard_normal((N, C, H, W)).astype(np.float32)
+    x[0, 0] = 0.0
+    x[0, 0, ::2, ::3] = -0.0
+    x[0, 1] = -np.float32(3.4028235e38)
+    x[0, 2] = -np.inf
+    x[0, 3, ::2] = np.nan
+    x[0, 4, 3:6, 3:6] = np.inf
+    x[1, 5] = np.nan
+    x[1, 6, :, 5] = 7.0
+    x[1, 7] = -0.0
+    x[1, 8:16] = np.round(x[1, 8:16])
+    rois = np.array([[b, x1, y1, x1 + w, y1 + h] for b in range(N) for (x1, y1, w, h) in
+                     [(0, 0, 13, 11), (1, 2, 5, 3), (3, 3, 0, 0), (2, 1, 9, 9), (-3, -2, 20, 20),
+                      (10, 8, 30, 30), (-20, -20, 5, 5)]], np.float32)
+    out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7,
+                                       rois_sorted=True)
+    oo, oa = orc.roi_pool_forward(x, rois, 7)
+    assert np.array_equal(am.cpu().numpy(), oa)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), oo.view(np.uint32))
