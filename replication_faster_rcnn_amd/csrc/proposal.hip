@@ -409,6 +409,7 @@ struct FusedShared {
     unsigned wsum[16];
     uint64_t red[16];
     uint64_t diag[64];
+    uint64_t keptw[16];
 };
 
 // Block-wide: find the bin d with cum(bins < d) < need <= cum(bins <= d).
@@ -483,11 +484,121 @@ __device__ uint64_t select_rank(const uint32_t (&sk)[KPT], int A, unsigned r, un
     return prefix;
 }
 
-template <int KPT>
+// ---------------------------------------------- hybrid first-chunk NMS
+// The lazy path below tests every 64-candidate block against the kept list on
+// the image's one CU.  The hybrid path (default) moves the first chunk's IoU
+// tests onto the whole chip:
+//   MODE 1 (one workgroup per image): select + sort the first kChunk
+//          candidates exactly as the lazy path does and hand them over (HybWs);
+//   chunk_colmask_kernel: every (row block, column block) tile of the chunk's
+//          upper triangle, lane = column: colT[j][w] bit i = row 64w+i (an
+//          earlier box) suppresses column j (torchvision's IoU test);
+//   MODE 2 (one workgroup per image): greedy sweep of the chunk from those
+//          bits (chunk_sweep), then the lazy path from the second chunk on --
+//          only if the first chunk kept fewer than post_nms boxes.
+struct HybWs {
+    float4* cbox;    // [N][kChunk] first-chunk boxes, score order
+    uint64_t* ckey;  // [N][kChunk] their keys (anchor index in the low word)
+    int* cc;         // [N] rows in the first chunk
+    int* P;          // [N] min(#valid, pre_nms)
+    uint64_t* colT;  // [N][kChunk][kChunkBlocks] column-form IoU bits
+};
+constexpr int kChunkBlocks = kChunk / 64;                           // 16
+constexpr int kChunkTiles = kChunkBlocks * (kChunkBlocks + 1) / 2;  // 136
+
+__global__ __launch_bounds__(64) void chunk_colmask_kernel(const float4* __restrict__ cbox_all,
+                                                           const int* __restrict__ cc_all, NmsThr thr,
+                                                           uint64_t* __restrict__ colT) {
+    const int n = blockIdx.y;
+    const int cc = cc_all[n];
+    const int nb = (cc + 63) / 64;
+    int rb, cb;
+    tri_tile(blockIdx.x, kChunkBlocks, rb, cb);
+    if (rb >= nb || cb >= nb) return;
+    const float4* cbox = cbox_all + static_cast<size_t>(n) * kChunk;
+    __shared__ float4 rbox[64];
+    __shared__ float rarea[64];
+    const int lane = threadIdx.x;
+    const int i0 = rb * 64;
+    if (i0 + lane < cc) {
+        const float4 b = cbox[i0 + lane];
+        rbox[lane] = b;
+        rarea[lane] = box_area(b);
+    }
+    __syncthreads();
+    const int j = cb * 64 + lane;
+    if (j >= cc) return;
+    const float4 bj = cbox[j];
+    const float aj = box_area(bj);
+    const int iend = min(min(64, cc - i0), j - i0);  // rows before column j
+    uint64_t bits = 0;
+    if (!thr.never) {
+#pragma unroll 4
+        for (int ii = 0; ii < iend; ++ii)
+            if (iou_over(rbox[ii], rarea[ii], bj, aj, thr)) bits |= 1ull << ii;
+    }
+    colT[(static_cast<size_t>(n) * kChunk + j) * kChunkBlocks + rb] = bits;
+}
+
+// Greedy NMS over the first chunk's rows [0, cc) from this image's colT.
+// Wave c holds the bits of columns [64c, 64c+64); blocks are resolved in
+// order, block b by wave b: avail = its columns not hit by a kept row of an
+// earlier block, then the fixed point K <- avail & ~{j : diag_j & K != 0}
+// (unique, = the greedy result); the later waves fold block b's kept set into
+// their hit flags.  Kept boxes go to kbox/karea and the outputs, at most post.
+__device__ int chunk_sweep(const uint64_t* __restrict__ colT, int cc, int post, const float4* cbox,
+                           const float* carea, const uint64_t* ckey, float4* kbox, float* karea,
+                           float4* orois, int32_t* oidx, FusedShared& sh) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int nb = (cc + 63) / 64;
+    const int j = wid * 64 + lane;
+    const bool jv = j < cc;
+    uint64_t col[kChunkBlocks];
+#pragma unroll
+    for (int w = 0; w < kChunkBlocks; ++w)
+        col[w] = (jv && w <= wid) ? colT[static_cast<size_t>(j) * kChunkBlocks + w] : 0ull;
+    bool hit = false;
+    int kcount = 0;
+#pragma unroll
+    for (int b = 0; b < kChunkBlocks; ++b) {
+        if (b >= nb || kcount >= post) break;
+        if (wid == b) {
+            const uint64_t avail = __ballot(jv && !hit);
+            const uint64_t diag = col[b];
+            uint64_t K = avail;
+            for (int it = 0; it < 65; ++it) {
+                const uint64_t Kn = avail & __ballot((diag & K) == 0ull);
+                if (Kn == K) break;
+                K = Kn;
+            }
+            const int room = post - kcount;
+            while (__popcll(K) > room) K &= ~(1ull << (63 - __clzll(K)));  // keep the first `room`
+            if ((K >> lane) & 1ull) {
+                const int slot = kcount + __popcll(K & lanemask_lt());
+                const float4 bx = cbox[j];
+                kbox[slot] = bx;
+                karea[slot] = carea[j];
+                orois[slot] = bx;
+                oidx[slot] = static_cast<int32_t>(static_cast<uint32_t>(ckey[j]));
+            }
+            if (lane == 0) sh.keptw[b] = K;
+        }
+        __syncthreads();
+        const uint64_t Kb = sh.keptw[b];
+        kcount += __popcll(Kb);
+        if (wid > b && (col[b] & Kb) != 0ull) hit = true;
+    }
+    __syncthreads();
+    return kcount;
+}
+
+// MODE 0: the lazy path, every chunk; MODE 1 / 2: the hybrid path's two
+// per-image halves (see above).
+template <int KPT, int MODE>
 __global__ __launch_bounds__(1024) void propose_fused_kernel(
     const uint64_t* __restrict__ keys_all, const float4* __restrict__ boxes_all, int A, int pre,
     int post, NmsThr thr, float4* __restrict__ out_rois, int32_t* __restrict__ out_idx,
-    int32_t* __restrict__ out_count) {
+    int32_t* __restrict__ out_count, HybWs hw) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     __shared__ FusedShared sh;
     unsigned* hist = reinterpret_cast<unsigned*>(lds_raw);                          // 16 KB
@@ -505,27 +616,50 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
     int32_t* oidx = out_idx + static_cast<size_t>(n) * post;
 
     uint32_t sk[KPT];
-    unsigned nv = 0;
-#pragma unroll
-    for (int k = 0; k < KPT; ++k) {
-        const int a = tid + k * 1024;
-        const uint64_t key = a < A ? keys[a] : kInvalidKey;
-        sk[k] = key == kInvalidKey ? 0xFFFFFFFFu : static_cast<uint32_t>(key >> 32);
-        nv += sk[k] != 0xFFFFFFFFu;
-    }
-    nv = wave_sum_u32(nv);
-    if (lane == 0) sh.wsum[wid] = nv;
-    if (tid == 0) sh.kcount = 0;
-    __syncthreads();
-    unsigned M = 0;
-    for (int w = 0; w < 16; ++w) M += sh.wsum[w];
-    const int P = static_cast<int>(M < static_cast<unsigned>(pre) ? M : static_cast<unsigned>(pre));
-    __syncthreads();
-
+    int P = 0;
     int r_done = 0;
     uint64_t T_prev = 0;
     bool have_prev = false;
     int kcount = 0;
+    if (MODE == 2) {  // first chunk: sorted by MODE 1, IoU bits from chunk_colmask_kernel
+        const int cc = hw.cc[n];
+        P = hw.P[n];
+        for (int i = tid; i < cc; i += 1024) {
+            const float4 b = hw.cbox[static_cast<size_t>(n) * kChunk + i];
+            cbox[i] = b;
+            carea[i] = box_area(b);
+            ckey[i] = hw.ckey[static_cast<size_t>(n) * kChunk + i];
+        }
+        __syncthreads();
+        kcount = chunk_sweep(hw.colT + static_cast<size_t>(n) * kChunk * kChunkBlocks, cc, post, cbox,
+                             carea, ckey, kbox, karea, orois, oidx, sh);
+        r_done = cc;
+        if (cc > 0) {
+            T_prev = ckey[cc - 1];
+            have_prev = true;
+        }
+        if (tid == 0) sh.kcount = kcount;
+    }
+    if (MODE != 2 || (kcount < post && r_done < P)) {  // the keys are needed (uniform)
+        unsigned nv = 0;
+#pragma unroll
+        for (int k = 0; k < KPT; ++k) {
+            const int a = tid + k * 1024;
+            const uint64_t key = a < A ? keys[a] : kInvalidKey;
+            sk[k] = key == kInvalidKey ? 0xFFFFFFFFu : static_cast<uint32_t>(key >> 32);
+            nv += sk[k] != 0xFFFFFFFFu;
+        }
+        if (MODE != 2) {
+            nv = wave_sum_u32(nv);
+            if (lane == 0) sh.wsum[wid] = nv;
+            if (tid == 0) sh.kcount = 0;
+            __syncthreads();
+            unsigned M = 0;
+            for (int w = 0; w < 16; ++w) M += sh.wsum[w];
+            P = static_cast<int>(M < static_cast<unsigned>(pre) ? M : static_cast<unsigned>(pre));
+        }
+        __syncthreads();
+    }
     while (r_done < P && kcount < post) {
         const int r_end = min(r_done + kChunk, P);
         const uint64_t T = select_rank<KPT>(sk, A, static_cast<unsigned>(r_end), hist, sh);
@@ -571,6 +705,17 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
             carea[tid] = box_area(b);
         }
         __syncthreads();
+        if (MODE == 1) {  // hand the sorted first chunk to chunk_colmask_kernel
+            if (tid < cc) {
+                hw.cbox[static_cast<size_t>(n) * kChunk + tid] = cbox[tid];
+                hw.ckey[static_cast<size_t>(n) * kChunk + tid] = key;
+            }
+            if (tid == 0) {
+                hw.cc[n] = cc;
+                hw.P[n] = P;
+            }
+            return;
+        }
         // ---- lazy NMS over 64-candidate blocks
         const int nb = (cc + 63) / 64;
 #pragma unroll 1
@@ -635,6 +780,13 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
         T_prev = T;
         have_prev = true;
     }
+    if (MODE == 1) {  // no valid candidate: an empty chunk
+        if (tid == 0) {
+            hw.cc[n] = 0;
+            hw.P[n] = P;
+        }
+        return;
+    }
     for (int s = kcount + tid; s < post; s += 1024) {
         orois[s] = make_float4(0.f, 0.f, 0.f, 0.f);
         oidx[s] = -1;
@@ -648,17 +800,30 @@ static size_t fused_lds_bytes(int post) {
 
 static int launch_fused(const uint64_t* keys, const float4* boxes, int N, int A, int pre, int post,
                         const NmsThr& thr, float4* out_rois, int32_t* out_idx, int32_t* out_count,
-                        hipStream_t st) {
+                        const HybWs& hw, bool lazy, hipStream_t st) {
     const size_t lds = fused_lds_bytes(post);
     const int kpt = (A + 1023) / 1024;
-#define FRCNN_FUSED(KP)                                                                         \
-    hipLaunchKernelGGL(propose_fused_kernel<KP>, dim3(N), dim3(1024), lds, st, keys, boxes, A, pre, \
-                       post, thr, out_rois, out_idx, out_count)
-    if (kpt <= 8) FRCNN_FUSED(8);
-    else if (kpt <= 16) FRCNN_FUSED(16);
-    else FRCNN_FUSED(24);
+#define FRCNN_FUSED(KP, MD)                                                                          \
+    hipLaunchKernelGGL((propose_fused_kernel<KP, MD>), dim3(N), dim3(1024), lds, st, keys, boxes, A, \
+                       pre, post, thr, out_rois, out_idx, out_count, hw)
+#define FRCNN_FUSED_KPT(MD)            \
+    if (kpt <= 8) FRCNN_FUSED(8, MD);  \
+    else if (kpt <= 16) FRCNN_FUSED(16, MD); \
+    else FRCNN_FUSED(24, MD)
+    if (lazy) {
+        FRCNN_FUSED_KPT(0);
+        FRCNN_LAUNCH_CHECK("propose_fused_kernel");
+        return FRCNN_OK;
+    }
+    FRCNN_FUSED_KPT(1);
+    FRCNN_LAUNCH_CHECK("propose_fused_kernel (first chunk)");
+    hipLaunchKernelGGL(chunk_colmask_kernel, dim3(kChunkTiles, N), dim3(64), 0, st, hw.cbox, hw.cc, thr,
+                       hw.colT);
+    FRCNN_LAUNCH_CHECK("chunk_colmask_kernel");
+    FRCNN_FUSED_KPT(2);
+    FRCNN_LAUNCH_CHECK("propose_fused_kernel (sweep)");
+#undef FRCNN_FUSED_KPT
 #undef FRCNN_FUSED
-    FRCNN_LAUNCH_CHECK("propose_fused_kernel");
     return FRCNN_OK;
 }
 
@@ -668,7 +833,7 @@ static int launch_fused(const uint64_t* keys, const float4* boxes, int N, int A,
 static bool use_fused(int N, int A, int post) {
     const char* force = getenv("FRCNN_PROPOSE_PATH");  // test / bench override
     if (A > kFusedMaxA || post > 4096) return false;
-    if (force && force[0] == 'f') return true;
+    if (force && (force[0] == 'f' || force[0] == 'l')) return true;  // fused hybrid / fused lazy
     if (force && force[0] == 'w') return false;
     return N >= 4 || post <= 1000;
 }
@@ -684,6 +849,7 @@ struct ProposeWs {
     float4* sbox;
     int32_t* sidx;
     uint64_t* maskT;
+    HybWs hyb;
     size_t bytes;
 };
 
@@ -700,6 +866,11 @@ static ProposeWs carve(void* ws, int N, int A, int pre, bool need_boxes) {
     w.sbox = c.take<float4>(static_cast<size_t>(N) * pre);
     w.sidx = c.take<int32_t>(static_cast<size_t>(N) * pre);
     w.maskT = c.take<uint64_t>(static_cast<size_t>(N) * Wc * pre);
+    w.hyb.cbox = c.take<float4>(static_cast<size_t>(N) * kChunk);
+    w.hyb.ckey = c.take<uint64_t>(static_cast<size_t>(N) * kChunk);
+    w.hyb.cc = c.take<int>(N);
+    w.hyb.P = c.take<int>(N);
+    w.hyb.colT = c.take<uint64_t>(static_cast<size_t>(N) * kChunk * kChunkBlocks);
     w.bytes = c.used();
     return w;
 }
@@ -778,9 +949,12 @@ extern "C" int frcnn_propose(const frcnn_propose_params* p, const float* scores,
                        reinterpret_cast<const float4*>(anchor_base), p->A, p->K, p->feat_w,
                        p->feat_stride, p->img_h, p->img_w, p->min_size, w.boxes, w.keys);
     FRCNN_LAUNCH_CHECK("decode_filter_kernel");
-    if (use_fused(p->N, p->A, p->post_nms))
+    if (use_fused(p->N, p->A, p->post_nms)) {
+        const char* force = getenv("FRCNN_PROPOSE_PATH");  // 'l': the lazy fused path (A/B, tests)
         return launch_fused(w.keys, w.boxes, p->N, p->A, pre, p->post_nms, make_thr(p->iou_threshold),
-                            reinterpret_cast<float4*>(out_rois), out_idx, out_count, st);
+                            reinterpret_cast<float4*>(out_rois), out_idx, out_count, w.hyb,
+                            force && force[0] == 'l', st);
+    }
     return sort_and_suppress(w, w.boxes, p->N, p->A, pre, p->post_nms, p->iou_threshold, 0,
                              reinterpret_cast<float4*>(out_rois), out_idx, nullptr, out_count, st);
 }

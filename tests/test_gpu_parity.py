@@ -20,9 +20,10 @@ DEV = "cuda"
 RTOL = 1e-5
 
 
-@pytest.fixture(params=["fused", "wide"])
+@pytest.fixture(params=["fused", "lazy", "wide"])
 def path(request, monkeypatch):
-    """Both proposal paths (fused per-image kernel / chip-wide bitmask NMS)."""
+    """The proposal paths: fused per-image with the chip-wide first-chunk mask
+    (default), fused lazy per-block, chip-wide bitmask NMS."""
     monkeypatch.setenv("FRCNN_PROPOSE_PATH", request.param)
     return request.param
 

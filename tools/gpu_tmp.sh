@@ -1,4 +1,5 @@
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "${PT_K:-roi_pool}" -x -q --timeout 120 --timeout-method thread > gpurun_out/pt.log 2>&1; rc=$?; tail -3 gpurun_out/pt.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python -u tools/ab_roi_pool.py --config cfg2 --variants ${AB_VARIANTS:-bal2,bal2ns,bal2c,bal2b,px8sorted} > gpurun_out/ab.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/ab.log; exit $rc
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pt.log 2>&1; rc=$?; tail -3 gpurun_out/pt.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python -u tools/ab_propose.py --config cfg2 > gpurun_out/abp.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/abp.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python -u tools/ab_propose.py --config cfg5 > gpurun_out/abp5.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/abp5.log; exit $rc
