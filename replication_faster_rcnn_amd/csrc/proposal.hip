@@ -496,6 +496,16 @@ __device__ uint64_t select_rank(const uint32_t (&sk)[KPT], int A, unsigned r, un
 //   MODE 2 (one workgroup per image): greedy sweep of the chunk from those
 //          bits (chunk_sweep), then the lazy path from the second chunk on --
 //          only if the first chunk kept fewer than post_nms boxes.
+// tools-only timeline probe (tools/prop_timeline.py): when g_prop_probe is set,
+// thread 0 of image n < 64 stamps s_memrealtime (100 MHz) at phase ends.
+__device__ int g_prop_probe;
+__device__ unsigned long long g_prop_dbg[64 * 16];
+#define FRCNN_PROBE(k)                                                                         \
+    do {                                                                                       \
+        if (probe && threadIdx.x == 0 && blockIdx.x < 64)                                      \
+            g_prop_dbg[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime();              \
+    } while (0)
+
 struct HybWs {
     float4* cbox;    // [N][kChunk] first-chunk boxes, score order
     uint64_t* ckey;  // [N][kChunk] their keys (anchor index in the low word)
@@ -506,9 +516,12 @@ struct HybWs {
 constexpr int kChunkBlocks = kChunk / 64;                           // 16
 constexpr int kChunkTiles = kChunkBlocks * (kChunkBlocks + 1) / 2;  // 136
 
-__global__ __launch_bounds__(64) void chunk_colmask_kernel(const float4* __restrict__ cbox_all,
-                                                           const int* __restrict__ cc_all, NmsThr thr,
-                                                           uint64_t* __restrict__ colT) {
+// 256 threads per tile: lane = column, wave w tests rows [16w, 16w+16) of the
+// row block (4 waves per tile keep the SIMDs busy; the tests are independent),
+// the four partial words are OR-ed in LDS.
+__global__ __launch_bounds__(256) void chunk_colmask_kernel(const float4* __restrict__ cbox_all,
+                                                            const int* __restrict__ cc_all, NmsThr thr,
+                                                            uint64_t* __restrict__ colT) {
     const int n = blockIdx.y;
     const int cc = cc_all[n];
     const int nb = (cc + 63) / 64;
@@ -518,26 +531,32 @@ __global__ __launch_bounds__(64) void chunk_colmask_kernel(const float4* __restr
     const float4* cbox = cbox_all + static_cast<size_t>(n) * kChunk;
     __shared__ float4 rbox[64];
     __shared__ float rarea[64];
-    const int lane = threadIdx.x;
+    __shared__ uint64_t part[4][64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int i0 = rb * 64;
-    if (i0 + lane < cc) {
-        const float4 b = cbox[i0 + lane];
-        rbox[lane] = b;
-        rarea[lane] = box_area(b);
+    if (tid < 64 && i0 + tid < cc) {
+        const float4 bx = cbox[i0 + tid];
+        rbox[tid] = bx;
+        rarea[tid] = box_area(bx);
     }
-    __syncthreads();
     const int j = cb * 64 + lane;
-    if (j >= cc) return;
-    const float4 bj = cbox[j];
+    const bool jv = j < cc;
+    const float4 bj = jv ? cbox[j] : make_float4(0.f, 0.f, 0.f, 0.f);
     const float aj = box_area(bj);
-    const int iend = min(min(64, cc - i0), j - i0);  // rows before column j
+    __syncthreads();
+    const int iend = jv ? min(min(64, cc - i0), j - i0) : 0;  // rows before column j
     uint64_t bits = 0;
     if (!thr.never) {
+        const int r0 = wid * 16;
 #pragma unroll 4
-        for (int ii = 0; ii < iend; ++ii)
-            if (iou_over(rbox[ii], rarea[ii], bj, aj, thr)) bits |= 1ull << ii;
+        for (int ii = r0; ii < r0 + 16; ++ii)
+            if (ii < iend && iou_over(rbox[ii], rarea[ii], bj, aj, thr)) bits |= 1ull << ii;
     }
-    colT[(static_cast<size_t>(n) * kChunk + j) * kChunkBlocks + rb] = bits;
+    part[wid][lane] = bits;
+    __syncthreads();
+    if (wid == 0 && jv)
+        colT[(static_cast<size_t>(n) * kChunk + j) * kChunkBlocks + rb] =
+            part[0][lane] | part[1][lane] | part[2][lane] | part[3][lane];
 }
 
 // Greedy NMS over the first chunk's rows [0, cc) from this image's colT.
@@ -610,6 +629,8 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
 
     const int n = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const bool probe = g_prop_probe != 0;
+    FRCNN_PROBE(MODE == 2 ? 8 : 0);
     const uint64_t* keys = keys_all + static_cast<size_t>(n) * A;
     const float4* boxes = boxes_all + static_cast<size_t>(n) * A;
     float4* orois = out_rois + static_cast<size_t>(n) * post;
@@ -631,6 +652,7 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
             ckey[i] = hw.ckey[static_cast<size_t>(n) * kChunk + i];
         }
         __syncthreads();
+        FRCNN_PROBE(9);
         kcount = chunk_sweep(hw.colT + static_cast<size_t>(n) * kChunk * kChunkBlocks, cc, post, cbox,
                              carea, ckey, kbox, karea, orois, oidx, sh);
         r_done = cc;
@@ -639,6 +661,7 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
             have_prev = true;
         }
         if (tid == 0) sh.kcount = kcount;
+        FRCNN_PROBE(10);
     }
     if (MODE != 2 || (kcount < post && r_done < P)) {  // the keys are needed (uniform)
         unsigned nv = 0;
@@ -659,12 +682,14 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
             P = static_cast<int>(M < static_cast<unsigned>(pre) ? M : static_cast<unsigned>(pre));
         }
         __syncthreads();
+        FRCNN_PROBE(1);
     }
     while (r_done < P && kcount < post) {
         const int r_end = min(r_done + kChunk, P);
         const uint64_t T = select_rank<KPT>(sk, A, static_cast<unsigned>(r_end), hist, sh);
         if (tid == 0) sh.ccount = 0;
         __syncthreads();
+        if (r_done == 0) FRCNN_PROBE(2);
 #pragma unroll
         for (int k = 0; k < KPT; ++k) {
             const int a = tid + k * 1024;
@@ -674,30 +699,43 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
             }
         }
         __syncthreads();
+        if (r_done == 0) FRCNN_PROBE(3);
         const int cc = r_end - r_done;  // == sh.ccount (keys are unique)
-        // ---- bitonic sort of the chunk, ascending
+        // ---- sort of the chunk, ascending: every wave bitonic-sorts its 64 keys
+        // with shuffles; a key's final position is its rank = the number of keys
+        // below it over the 16 sorted runs (binary searches; valid keys are
+        // distinct, the invalid padding sorts last and is not placed)
         uint64_t key = tid < cc ? ckey[tid] : kInvalidKey;
-#pragma unroll 1
-        for (int kk = 2; kk <= kChunk; kk <<= 1) {
-#pragma unroll 1
+        for (int kk = 2; kk <= 64; kk <<= 1) {
             for (int j = kk >> 1; j > 0; j >>= 1) {
-                uint64_t other;
-                if (j >= 64) {
-                    __syncthreads();
-                    ckey[tid] = key;
-                    __syncthreads();
-                    other = ckey[tid ^ j];
-                } else {
-                    other = __shfl_xor(key, j, 64);
-                }
-                const bool asc = (tid & kk) == 0;
-                const bool lower = (tid & j) == 0;
+                const uint64_t other = __shfl_xor(key, j, 64);
+                const bool asc = (lane & kk) == 0;
+                const bool lower = (lane & j) == 0;
                 const uint64_t mn = other < key ? other : key;
                 const uint64_t mx = other < key ? key : other;
                 key = (lower == asc) ? mn : mx;
             }
         }
+        __syncthreads();  // the reads of ckey above are done
+        ckey[tid] = key;
         __syncthreads();
+        int rank = lane;  // within its own run
+#pragma unroll
+        for (int w = 0; w < kChunk / 64; ++w) {
+            if (w == wid) continue;
+            const uint64_t* run = ckey + w * 64;
+            int lo = 0;
+#pragma unroll
+            for (int step = 32; step > 0; step >>= 1)
+                if (run[lo + step - 1] < key) lo += step;
+            lo += run[lo] < key ? 1 : 0;
+            rank += lo;
+        }
+        __syncthreads();
+        if (key != kInvalidKey) ckey[rank] = key;
+        __syncthreads();
+        key = ckey[tid];
+        if (r_done == 0) FRCNN_PROBE(4);
         ckey[tid] = key;
         if (tid < cc) {
             const float4 b = boxes[static_cast<uint32_t>(key)];
@@ -705,6 +743,7 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
             carea[tid] = box_area(b);
         }
         __syncthreads();
+        if (r_done == 0) FRCNN_PROBE(5);
         if (MODE == 1) {  // hand the sorted first chunk to chunk_colmask_kernel
             if (tid < cc) {
                 hw.cbox[static_cast<size_t>(n) * kChunk + tid] = cbox[tid];
@@ -714,6 +753,7 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
                 hw.cc[n] = cc;
                 hw.P[n] = P;
             }
+            FRCNN_PROBE(6);
             return;
         }
         // ---- lazy NMS over 64-candidate blocks
@@ -792,6 +832,7 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
         oidx[s] = -1;
     }
     if (tid == 0) out_count[n] = kcount;
+    FRCNN_PROBE(MODE == 2 ? 11 : 7);
 }
 
 static size_t fused_lds_bytes(int post) {
@@ -817,7 +858,7 @@ static int launch_fused(const uint64_t* keys, const float4* boxes, int N, int A,
     }
     FRCNN_FUSED_KPT(1);
     FRCNN_LAUNCH_CHECK("propose_fused_kernel (first chunk)");
-    hipLaunchKernelGGL(chunk_colmask_kernel, dim3(kChunkTiles, N), dim3(64), 0, st, hw.cbox, hw.cc, thr,
+    hipLaunchKernelGGL(chunk_colmask_kernel, dim3(kChunkTiles, N), dim3(256), 0, st, hw.cbox, hw.cc, thr,
                        hw.colT);
     FRCNN_LAUNCH_CHECK("chunk_colmask_kernel");
     FRCNN_FUSED_KPT(2);
@@ -984,4 +1025,13 @@ extern "C" int frcnn_nms(const float* boxes, const float* scores, int64_t n, dou
     FRCNN_LAUNCH_CHECK("nms_keys_kernel");
     return sort_and_suppress(w, reinterpret_cast<const float4*>(boxes), 1, N, N, N, iou_threshold,
                              1, nullptr, nullptr, keep, count, st);
+}
+
+// tools-only (not part of the C-ABI): switch the proposal timeline probe and read it
+extern "C" int frcnn_dbg_prop_probe(int on) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_prop_probe), &on, sizeof(int)) == hipSuccess ? 0 : -2;
+}
+extern "C" int frcnn_dbg_prop_stamps(unsigned long long* host, int n) {
+    if (n > 64 * 16) n = 64 * 16;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_prop_dbg), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -2;
 }
