@@ -7,7 +7,7 @@ input already resident in HBM (BASELINE.json configs[1] = cfg2: 8 images of
 600x1000, stride-16 38x63x9 anchors, 6000->300 NMS@0.7, RoIPool 7x7x256):
 
     propose (decode+clamp+filter+top-k+NMS+post, anchors generated in-kernel)
-    -> RoI transform (nets/heads.py:42-47) -> RoIPool forward
+    -> RoI transform + pack + RoIPool forward (nets/heads.py:42-48, one launch)
 
 For N>1 (torch.distributed.run, one process per GPU) every rank runs its own
 batch of 8 images (weak scaling, images seeded by global index) and the
@@ -15,8 +15,8 @@ padded detections are all-gathered over RCCL at the end of each step -- the
 only collective on this path.
 
 Prints ONE JSON line (rank 0) with the metric of BASELINE.json plus
-"roofline" (RoIPool forward, achieved algorithmic HBM GB/s from HIP events
-vs the 8 TB/s peak) and "cpu_baseline" (the oracle CPU path on this host).
+"roofline" (the RoIPool forward launch, achieved algorithmic HBM GB/s from
+HIP events on the launch stream vs the 8 TB/s peak) and "cpu_baseline" (the oracle CPU path on this host).
 """
 from __future__ import annotations
 
@@ -123,12 +123,12 @@ def main():
         rois, idx, cnt = ops.propose(sc, de, img_w=c["img_w"], img_h=c["img_h"],
                                      pre_nms=c["pre_nms"], post_nms=post, anchor_base=base,
                                      feat_h=c["feat_h"], feat_w=c["feat_w"])
-        boxes = ops.roi_transform(rois.view(-1, 4), inds, c["img_h"], c["img_w"], c["feat_h"],
-                                  c["feat_w"])
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        pooled, am = ops._roi_pool_fwd(x, boxes, 7, 7, 1.0, rois_sorted=True)
+        # ResnetHead's transform + pack + roi_pool (nets/heads.py:42-48): one launch
+        pooled, am, boxes = ops.roi_pool_head(x, rois.view(-1, 4), inds, 7, c["img_h"], c["img_w"],
+                                              rois_sorted=True)
         if timed:
             e1.record()
             ev.append((e0, e1))
@@ -174,7 +174,7 @@ def main():
                    "global_batch": world * N, "parallelism": f"dp{world} (per-image sharding)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "roi_pool_fwd_kernel", "kernel_us": roi_ms * 1e3,
+                     "kernel": "roi_pool_fwd_px8q_kernel<head>", "kernel_us": roi_ms * 1e3,
                      "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": None,
     }

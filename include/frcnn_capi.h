@@ -105,14 +105,28 @@ int frcnn_roi_transform(const float* rois, const float* roi_inds, int64_t R, flo
  *   x fp32 [N,C,H,W], rois fp32 [R,5] -> out fp32 [R,C,PH,PW],
  *   argmax int32 [R,C,PH,PW] (h*W+w within the plane, -1 for empty bins).
  * RoIs whose batch index is outside [0,N) produce 0 / -1.
- * rois_sorted != 0 says the RoIs are grouped by batch index (true for
- * proposals and for train.py's sample_rois_ind): a cost-balanced two-launch
- * path (partition + pool); the result is exact for any order either way.
+ * rois_sorted != 0 PROMISES the RoIs are grouped by non-decreasing batch
+ * index (true for proposals and for train.py's sample_rois_ind): one launch,
+ * each workgroup finds its image's RoI range itself.  rois_sorted == 0 works
+ * for any order (a list kernel groups them first).
  * The workspace (frcnn_roi_pool_fwd_workspace_size bytes) is always required. */
 size_t frcnn_roi_pool_fwd_workspace_size(int64_t R, int N, int C);
 int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
                        int PH, int PW, float spatial_scale, int rois_sorted, float* out,
                        int32_t* argmax, void* workspace, size_t ws_bytes, void* stream);
+
+/* ResnetHead.forward's RoI transform + pack + roi_pool (nets/heads.py:42-48)
+ * in one call: rois fp32 [R,4] in image pixels (RPN output / sample_rois),
+ * roi_inds fp32 [R] -> boxes fp32 [R,5] exactly as frcnn_roi_transform, and
+ * out / argmax exactly as frcnn_roi_pool_fwd on those boxes.  With
+ * rois_sorted != 0 (same promise as above) the transform runs inside the pool
+ * kernel (one launch); otherwise the two calls run back to back.  boxes is
+ * always written (the backward needs it).  Workspace: frcnn_roi_pool_fwd_
+ * workspace_size(R, N, C). */
+int frcnn_roi_pool_fwd_head(const float* x, const float* rois, const float* roi_inds, int64_t R,
+                            int N, int C, int H, int W, int PH, int PW, float img_h, float img_w,
+                            float spatial_scale, int rois_sorted, float* boxes, float* out,
+                            int32_t* argmax, void* workspace, size_t ws_bytes, void* stream);
 
 /* torchvision _roi_pool_backward (autograd of nets/heads.py:48, reached from
  * train.py:126):  grad_in fp32 [N,C,H,W] = 0, then for n, c, ph, pw in order

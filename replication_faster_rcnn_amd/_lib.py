@@ -49,6 +49,8 @@ SIGNATURES = {
     "frcnn_roi_transform": (I32, [P, P, I64, F32, F32, I32, I32, P, P]),
     "frcnn_roi_pool_fwd_workspace_size": (SZ, [I64, I32, I32]),
     "frcnn_roi_pool_fwd": (I32, [P, P, I64, I32, I32, I32, I32, I32, I32, F32, I32, P, P, P, SZ, P]),
+    "frcnn_roi_pool_fwd_head": (I32, [P, P, P, I64, I32, I32, I32, I32, I32, I32, F32, F32, F32, I32,
+                                      P, P, P, P, SZ, P]),
     "frcnn_roi_pool_bwd_workspace_size": (SZ, [I64, I32, I32, I32]),
     "frcnn_roi_pool_bwd": (I32, [P, P, P, I64, I32, I32, I32, I32, I32, I32, F32, P, P, SZ, P]),
     "frcnn_bbox_iou": (I32, [P, I32, I64, P, I32, I64, P, P]),

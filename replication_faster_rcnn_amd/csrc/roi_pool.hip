@@ -338,10 +338,10 @@ __global__ __launch_bounds__(kTileThreads) void roi_pool_fwd_wave_kernel(
 // non-decreasing batch index: image b's RoIs are then [count(<b), count(<b+1)).
 template <int NT>
 __device__ __forceinline__ int2 roi_range_sorted(const float* __restrict__ rois, int R, int b0,
-                                                 int b1, int* red) {
+                                                 int b1, int* red, int stride = 5) {
     int c0 = 0, c1 = 0;
     for (int r = threadIdx.x; r < R; r += NT) {
-        const int rb = static_cast<int>(rois[static_cast<size_t>(r) * 5]);
+        const int rb = static_cast<int>(rois[static_cast<size_t>(r) * stride]);
         c0 += rb < b0;
         c1 += rb < b1;
     }
@@ -463,6 +463,316 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_px8_kernel(
             }
         }
         t = __builtin_amdgcn_readfirstlane(tn);
+    }
+}
+
+// Strict '>' update of 8 running (max, first index) pairs with one pixel.
+__device__ __forceinline__ void take8(const float4& a, const float4& b, int ii, float (&mv)[8],
+                                      int (&mi)[8]) {
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        if (v[c] > mv[c]) {
+            mv[c] = v[c];
+            mi[c] = ii;
+        }
+    }
+}
+
+// px8q: px8 for image-grouped RoIs with
+//  * a split-plane LDS tile: lo[s] = channels 0-3, hi[s] = channels 4-7 of
+//    pixel p in slot s = p ^ ((p >> 4) & 15) (an XOR swizzle inside each
+//    aligned 16-pixel group; the tile is padded to a multiple of 16 pixels).
+//    A ds_read_b128 serves 16 lanes per LDS cycle on 16-B bank groups
+//    ((a/16) mod 16); bins of one bin row sit a bin width apart, which in the
+//    32-B interleaved px8 tile collide every 8 pixels -- here only within a
+//    16-pixel group, and the swizzle scatters strides that cross groups;
+//  * staging one pixel (8 channels) per thread: 8 coalesced global loads, two
+//    ds_write_b128 (px8's strided ds_write_b32 is 8-way bank-conflicted);
+//  * a strided RoI share: workgroup z of `split` takes items z, z+split, ...
+//    of its image (RoI sizes are uncorrelated with rank, so every share sees
+//    the image's size mix);
+//  * CG = 16 (when 16 channel planes fit the CU's LDS, one workgroup per CU):
+//    the RoI geometry, the window walk and the per-pixel address are shared by
+//    16 channels instead of 8 -- the scan is VALU-issue bound, and these are a
+//    third of its instructions at CG = 8.  Planes of 4 channels each.
+// HEAD: fused with the head's RoI transform (nets/heads.py:42-47): `rois` are
+// the RPN / sampler boxes [R,4] in image pixels, `hd.inds` their image index
+// [R]; the [idx, box] pack is formed in registers (the same fp32 divide-then-
+// multiply as roi_transform_kernel) and, when hd.boxes is set, written out
+// once (channel group 0) for the backward.
+struct HeadArgs {
+    const float* inds;
+    float img_h, img_w, fh, fw;
+    float* boxes;
+};
+
+template <int NT, int CG, int MODE = 0, bool HEAD = false, bool SWZ = true>  // MODE (tools only): 1 = no stores, 2 = no window scan
+__global__ __launch_bounds__(NT) void roi_pool_fwd_px8q_kernel(
+    const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W,
+    int PH, int PW, float ss, float* __restrict__ out, int32_t* __restrict__ argmax, int geo_cap,
+    HeadArgs hd = HeadArgs{}) {
+    constexpr int NP = CG / 4;                                     // planes of 4 channels
+    extern __shared__ __attribute__((aligned(16))) float4 q4[];  // plane k at q4 + k * HWs; geometry after
+    __shared__ int s_red[2 * (NT / 64)];
+    __shared__ int s_next;
+    const int b = blockIdx.y;
+    const int c0 = blockIdx.x * CG;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int HW = H * W;
+    const int HWs = (HW + 15) & ~15;
+    const int PHW = PH * PW;
+    const int split = gridDim.z, z = blockIdx.z;
+    const int N = gridDim.y - 1;
+    if (b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
+        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, 0, N, s_red, 1)
+                             : roi_range_sorted<NT>(rois, R, 0, N, s_red);
+        const int n_lo = rg.x, n_hi = R - rg.y, tot = n_lo + n_hi;
+        const int lo = static_cast<int>(static_cast<int64_t>(tot) * z / split);
+        const int hi = static_cast<int>(static_cast<int64_t>(tot) * (z + 1) / split);
+        if (HEAD && hd.boxes && blockIdx.x == 0)
+            for (int t = lo + tid; t < hi; t += NT) {
+                const int r = t < n_lo ? t : rg.y + (t - n_lo);
+                const float4 v = reinterpret_cast<const float4*>(rois)[r];
+                float* o = hd.boxes + static_cast<size_t>(r) * 5;
+                o[0] = hd.inds[r];
+                o[1] = v.x / hd.img_h * hd.fh;
+                o[2] = v.y / hd.img_w * hd.fw;
+                o[3] = v.z / hd.img_h * hd.fh;
+                o[4] = v.w / hd.img_w * hd.fw;
+            }
+        for (int e = lo * CG * PHW + tid; e < hi * CG * PHW; e += NT) {
+            const int t = e / (CG * PHW);
+            const int rem = e - t * (CG * PHW);
+            const int r = t < n_lo ? t : rg.y + (t - n_lo);
+            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + rem;
+            out[o] = 0.0f;
+            argmax[o] = -1;
+        }
+        return;
+    }
+    const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, b, b + 1, s_red, 1)
+                         : roi_range_sorted<NT>(rois, R, b, b + 1, s_red);
+    const int rbase = rg.x, nr = rg.y - rg.x;
+    if (z >= nr) return;
+    const int nmine = (nr - z + split - 1) / split;  // items z, z+split, ...
+    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+    for (int p = tid; p < HW; p += NT) {
+        float v[CG];
+#pragma unroll
+        for (int q = 0; q < CG; ++q) v[q] = src[static_cast<size_t>(q) * HW + p];
+        const int s = SWZ ? p ^ ((p >> 4) & 15) : p;
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            q4[k * HWs + s] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    }
+    // RoI geometry (sh, sw, bin_h, bin_w) of up to geo_cap items at a time, computed
+    // once per workgroup instead of once per wave: the rounds and the IEEE divides
+    // (and, for HEAD, the transform's) are a fifth of a small RoI's VALU work.
+    int4* s_geo = reinterpret_cast<int4*>(q4 + NP * HWs);
+    const int ph = lane / PW, pw = lane - (lane / PW) * PW;
+    const bool act = lane < PHW;
+    for (int k0 = 0; k0 < nmine; k0 += geo_cap) {
+        const int cn = min(geo_cap, nmine - k0);
+        for (int i = tid; i < cn; i += NT) {
+            const int r = rbase + z + (k0 + i) * split;
+            RoiGeom gm;
+            if (HEAD) {
+                const float4 v = reinterpret_cast<const float4*>(rois)[r];
+                const float bx[5] = {hd.inds[r], v.x / hd.img_h * hd.fh, v.y / hd.img_w * hd.fw,
+                                     v.z / hd.img_h * hd.fh, v.w / hd.img_w * hd.fw};
+                gm = roi_geom(bx, ss, PH, PW);
+                if (hd.boxes && blockIdx.x == 0) {
+                    float* o = hd.boxes + static_cast<size_t>(r) * 5;
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) o[j] = bx[j];
+                }
+            } else {
+                gm = roi_geom(rois + static_cast<size_t>(r) * 5, ss, PH, PW);
+            }
+            s_geo[i] = make_int4(gm.sh, gm.sw, __float_as_int(gm.bh), __float_as_int(gm.bw));
+        }
+        if (tid == 0) s_next = 0;
+        __syncthreads();
+        int k = 0;
+        if (lane == 0) k = atomicAdd(&s_next, 1);
+        k = __builtin_amdgcn_readfirstlane(k);
+        while (k < cn) {
+            int kn = 0;
+            if (lane == 0) kn = atomicAdd(&s_next, 1);  // prefetch the next item
+            const int r = rbase + z + (k0 + k) * split;
+            const int4 gq = s_geo[k];
+            RoiGeom gm;
+            gm.sh = gq.x;
+            gm.sw = gq.y;
+            gm.bh = __int_as_float(gq.z);
+            gm.bw = __int_as_float(gq.w);
+            int4 g = geom_bin(gm, H, W, ph, pw);
+            if (!act) g = make_int4(0, 0, 0, 0);
+            const bool empty = g.y <= g.x || g.w <= g.z;
+            float mv[CG];
+            int mi[CG];
+#pragma unroll
+            for (int c = 0; c < CG; ++c) {
+                mv[c] = empty ? 0.0f : -FLT_MAX;
+                mi[c] = -1;
+            }
+            for (int h = g.x; h < (MODE == 2 ? g.x : g.y); ++h) {
+                const int rb = h * W;
+                for (int w = g.z; w < g.w; ++w) {
+                    const int ii = rb + w;
+                    const int s = SWZ ? ii ^ ((ii >> 4) & 15) : ii;
+                    float4 v[NP];
+#pragma unroll
+                    for (int q = 0; q < NP; ++q) v[q] = q4[q * HWs + s];
+#pragma unroll
+                    for (int q = 0; q < NP; ++q) {
+                        const float vv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            if (vv[j] > mv[4 * q + j]) {  // torchvision's strict '>'
+                                mv[4 * q + j] = vv[j];
+                                mi[4 * q + j] = ii;
+                            }
+                        }
+                    }
+                }
+            }
+            if (act && (MODE != 1 || mv[0] == 1234.5f)) {
+                const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
+#pragma unroll
+                for (int c = 0; c < CG; ++c) {
+                    out[o + static_cast<size_t>(c) * PHW] = mv[c];
+                    argmax[o + static_cast<size_t>(c) * PHW] = mi[c];
+                }
+            }
+            k = __builtin_amdgcn_readfirstlane(kn);
+        }
+        __syncthreads();  // the chunk's geometry and s_next are reused
+    }
+}
+
+__device__ __forceinline__ float nan_to_ninf(float v) { return v != v ? -INFINITY : v; }
+
+// px8r: the px8q work split with fewer VALU per channel-pixel.
+//  * Tile: two planes, lo[p] = channels 0-3, hi[p] = channels 4-7 of pixel p
+//    (no swizzle: one address per pixel, stepped by 16 B; hi at a fixed
+//    ds_read offset).  NaN is staged as -inf: neither ever passes the
+//    reference's strict '>' against the -FLT_MAX start, so the result is the
+//    same, and v_max3 never sees a NaN.
+//  * Pixels are taken in row-major pairs (a, b) (b clamped to the row end: a
+//    revisit of a is harmless).  Per channel: m' = max3(m, a, b); if m' > m the
+//    max moved into the pair, to a if a == m' (a first), else to b.  That is
+//    the strict-'>' first-max scan exactly (a tie with m never moves it), at
+//    5 VALU per pair instead of 6; a shared pair of indices, one address.
+//  * The kept value is m' from max3, which may differ from the first max in
+//    the sign of a zero; the final value is re-read from the tile at the
+//    argmax when it compares equal to 0.
+__device__ __forceinline__ void take8_pair(const float4& a0, const float4& a1, const float4& b0,
+                                           const float4& b1, int ia, int ib, float (&mv)[8],
+                                           int (&mi)[8]) {
+    const float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        const float m2 = __builtin_fmaxf(__builtin_fmaxf(mv[c], a[c]), b[c]);
+        const int ip = a[c] == m2 ? ia : ib;
+        if (m2 > mv[c]) mi[c] = ip;
+        mv[c] = m2;
+    }
+}
+
+template <int NT, int MODE = 0>  // MODE (tools only): 1 = no stores
+__global__ __launch_bounds__(NT) void roi_pool_fwd_px8r_kernel(
+    const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W,
+    int PH, int PW, float ss, float* __restrict__ out, int32_t* __restrict__ argmax) {
+    constexpr int CG = 8;
+    extern __shared__ __attribute__((aligned(16))) float4 r4[];  // lo[HW] then hi[HW]
+    __shared__ int s_red[2 * (NT / 64)];
+    __shared__ int s_next;
+    const int b = blockIdx.y;
+    const int c0 = blockIdx.x * CG;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int HW = H * W;
+    const int PHW = PH * PW;
+    const int split = gridDim.z, z = blockIdx.z;
+    const int N = gridDim.y - 1;
+    if (b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
+        const int2 rg = roi_range_sorted<NT>(rois, R, 0, N, s_red);
+        const int n_lo = rg.x, n_hi = R - rg.y, tot = n_lo + n_hi;
+        const int lo = static_cast<int>(static_cast<int64_t>(tot) * z / split);
+        const int hi = static_cast<int>(static_cast<int64_t>(tot) * (z + 1) / split);
+        for (int e = lo * CG * PHW + tid; e < hi * CG * PHW; e += NT) {
+            const int t = e / (CG * PHW);
+            const int rem = e - t * (CG * PHW);
+            const int r = t < n_lo ? t : rg.y + (t - n_lo);
+            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + rem;
+            out[o] = 0.0f;
+            argmax[o] = -1;
+        }
+        return;
+    }
+    const int2 rg = roi_range_sorted<NT>(rois, R, b, b + 1, s_red);
+    const int rbase = rg.x, nr = rg.y - rg.x;
+    if (z >= nr) return;
+    const int nmine = (nr - z + split - 1) / split;  // items z, z+split, ...
+    if (tid == 0) s_next = 0;
+    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+    for (int p = tid; p < HW; p += NT) {
+        float v[CG];
+#pragma unroll
+        for (int q = 0; q < CG; ++q) v[q] = nan_to_ninf(src[static_cast<size_t>(q) * HW + p]);
+        r4[p] = make_float4(v[0], v[1], v[2], v[3]);
+        r4[HW + p] = make_float4(v[4], v[5], v[6], v[7]);
+    }
+    __syncthreads();
+    const char* tb = reinterpret_cast<const char*>(r4);
+    const int hoff = HW * 16;
+    const int ph = lane / PW, pw = lane - (lane / PW) * PW;
+    const bool act = lane < PHW;
+    int k = 0;
+    if (lane == 0) k = atomicAdd(&s_next, 1);
+    k = __builtin_amdgcn_readfirstlane(k);
+    while (k < nmine) {
+        int kn = 0;
+        if (lane == 0) kn = atomicAdd(&s_next, 1);  // prefetch the next item
+        const int r = rbase + z + k * split;
+        const RoiGeom gm = roi_geom(rois + static_cast<size_t>(r) * 5, ss, PH, PW);
+        int4 g = geom_bin(gm, H, W, ph, pw);
+        if (!act) g = make_int4(0, 0, 0, 0);
+        const bool empty = g.y <= g.x || g.w <= g.z;
+        float mv[CG];
+        int mi[CG];
+#pragma unroll
+        for (int c = 0; c < CG; ++c) {
+            mv[c] = empty ? 0.0f : -FLT_MAX;
+            mi[c] = -1;
+        }
+        const int wlast = g.w - 1;
+        for (int h = g.x; h < g.y; ++h) {
+            const int rb = h * W;
+            for (int w = g.z; w < g.w; w += 2) {
+                const int ia = rb + w, ib = rb + min(w + 1, wlast);
+                const float4 a0 = *reinterpret_cast<const float4*>(tb + ia * 16);
+                const float4 a1 = *reinterpret_cast<const float4*>(tb + hoff + ia * 16);
+                const float4 b0 = *reinterpret_cast<const float4*>(tb + ib * 16);
+                const float4 b1 = *reinterpret_cast<const float4*>(tb + hoff + ib * 16);
+                take8_pair(a0, a1, b0, b1, ia, ib, mv, mi);
+            }
+        }
+        if (act && (MODE != 1 || mv[0] == 1234.5f)) {
+            const float* tf = reinterpret_cast<const float*>(r4);
+#pragma unroll
+            for (int c = 0; c < CG; ++c)  // exact bits of a zero maximum
+                if (mv[c] == 0.0f && mi[c] >= 0) mv[c] = tf[(c < 4 ? 0 : 4 * HW) + 4 * mi[c] + (c & 3)];
+            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
+#pragma unroll
+            for (int c = 0; c < CG; ++c) {
+                out[o + static_cast<size_t>(c) * PHW] = mv[c];
+                argmax[o + static_cast<size_t>(c) * PHW] = mi[c];
+            }
+        }
+        k = __builtin_amdgcn_readfirstlane(kn);
     }
 }
 
@@ -759,19 +1069,6 @@ __device__ __forceinline__ int wave_max_i32(int v) {
     return __builtin_amdgcn_readfirstlane(v);
 }
 
-// Strict '>' update of 8 running (max, first index) pairs with one pixel.
-__device__ __forceinline__ void take8(const float4& a, const float4& b, int ii, float (&mv)[8],
-                                      int (&mi)[8]) {
-    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        if (v[c] > mv[c]) {
-            mv[c] = v[c];
-            mi[c] = ii;
-        }
-    }
-}
-
 template <int NT, int FIX, bool SWAP, int MODE>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8, 8))) void roi_pool_fwd_bal2_kernel(
     const float* __restrict__ x, const float* __restrict__ rois, const int* __restrict__ seg_lo,
@@ -1035,7 +1332,6 @@ __global__ __launch_bounds__(kTileThreads) void roi_pool_fwd_pxf_kernel(
 //           and the output value (its exact bits, e.g. -0.0 vs +0.0).
 // NaN never wins in the reference; it is staged into LDS as -inf, which never
 // wins either.  A max not above init means "nothing selected": (init, -1).
-__device__ __forceinline__ float nan_to_ninf(float v) { return v != v ? -INFINITY : v; }
 
 __global__ __launch_bounds__(kTileThreads) void roi_pool_fwd_px8s_kernel(
     const float* __restrict__ x, const float* __restrict__ rois, const int* __restrict__ list,
@@ -1332,8 +1628,10 @@ constexpr int kFwdCG = 4;                       // channels per image tile
 constexpr size_t kFwdTileBudget = 96 * 1024;    // LDS for the CG planes
 constexpr size_t kLdsPerCu = 160 * 1024;        // gfx950
 constexpr size_t kBalStatic = 1024;             // static LDS of the balanced kernel (rounded up)
-// default forward for image-grouped RoIs: 0 = px8 (count split), 2 = balanced v2
-constexpr int kSortedDefault = 0;
+// default forward for image-grouped RoIs: px8q (px_plan: 16- or 8-channel
+// swizzled planes, strided shares); 0 = px8 (count split), 2 = balanced v2
+// are the A/B alternatives
+constexpr int kSortedDefault = 1;
 
 int device_cu_count();
 // segments of the balanced forward: at most two resident workgroups per CU
@@ -1363,7 +1661,72 @@ int device_cu_count() {
     }
     return cus;
 }
+// Launch plan of the image-tile forward (roi_pool_fwd_px8q_kernel) for RoIs
+// grouped by image: CG = 16 channel planes when they fit the CU's LDS (one
+// workgroup per CU), else 8 (two per CU when they fit).  Each workgroup gets
+// the LDS left over for its RoI-geometry chunk; split = RoI shares per
+// (image, channel group), sized so the grid fills every resident slot once.
+struct PxPlan {
+    int cg = 0, geo_cap = 0, split = 1, N = 0;
+    size_t lds = 0;
+};
+PxPlan px_plan(int C, int N, int H, int W, int PH, int PW, int want_cg) {
+    PxPlan pl;
+    const size_t HW = static_cast<size_t>(H) * W;
+    if (N <= 0 || HW == 0 || PH * PW > 64 || H > 65535 || W > 65535) return pl;
+    constexpr size_t kReserve = 1024;  // static LDS + allocation rounding
+    constexpr size_t kMinGeo = 64 * sizeof(int4);
+    const size_t HWs = (HW + 15) & ~static_cast<size_t>(15);
+    for (int cg : {16, 8}) {
+        if ((want_cg && cg != want_cg) || C % cg != 0) continue;
+        const size_t tile = static_cast<size_t>(cg / 4) * HWs * sizeof(float4);
+        int per_cu = 0;
+        if (2 * (tile + kMinGeo + kReserve) <= kLdsPerCu) per_cu = 2;
+        else if (tile + kMinGeo + kReserve <= kLdsPerCu) per_cu = 1;
+        if (!per_cu) continue;
+        size_t geo = (kLdsPerCu / per_cu - kReserve - tile) / sizeof(int4);
+        pl.geo_cap = static_cast<int>(geo > 512 ? 512 : geo);
+        pl.cg = cg;
+        pl.lds = tile + static_cast<size_t>(pl.geo_cap) * sizeof(int4);
+        const int64_t wgs = static_cast<int64_t>(C / cg) * N;
+        const int64_t target = static_cast<int64_t>(device_cu_count()) * per_cu;
+        int64_t sp = (target + wgs - 1) / wgs;
+        if (const char* e = getenv("FRCNN_ROIPOOL_SPLIT")) sp = std::atoi(e);  // A/B override
+        pl.split = static_cast<int>(sp < 1 ? 1 : (sp > 64 ? 64 : sp));
+        pl.N = N;
+        return pl;
+    }
+    return pl;
+}
+
+int px_launch(const PxPlan& pl, int mode, const float* x, const float* rois, int64_t R, int C, int H,
+              int W, int PH, int PW, float ss, float* out, int32_t* argmax, const HeadArgs& hd,
+              hipStream_t st) {
+    const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(pl.N + 1),
+                    static_cast<unsigned>(pl.split));
+    const bool head = hd.inds != nullptr;
+#define FRCNN_PX(CG, MD, HD)                                                                          \
+    hipLaunchKernelGGL((roi_pool_fwd_px8q_kernel<1024, CG, MD, HD>), grid, dim3(1024), pl.lds, st, x, \
+                       rois, static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd)
+    if (pl.cg == 16) {
+        if (head) FRCNN_PX(16, 0, true);
+        else if (mode == 3) hipLaunchKernelGGL((roi_pool_fwd_px8q_kernel<1024, 16, 0, false, false>), grid, dim3(1024),
+                                               pl.lds, st, x, rois, static_cast<int>(R), C, H, W, PH, PW, ss, out,
+                                               argmax, pl.geo_cap, hd);
+        else if (mode == 1) FRCNN_PX(16, 1, false);
+        else FRCNN_PX(16, 0, false);
+    } else {
+        if (head) FRCNN_PX(8, 0, true);
+        else if (mode == 1) FRCNN_PX(8, 1, false);
+        else if (mode == 2) FRCNN_PX(8, 2, false);
+        else FRCNN_PX(8, 0, false);
+    }
+#undef FRCNN_PX
+    FRCNN_LAUNCH_CHECK("roi_pool_fwd_px8q_kernel");
+    return FRCNN_OK;
+}
 }  // namespace
+
 
 extern "C" size_t frcnn_roi_pool_fwd_workspace_size(int64_t R, int N, int C) {
     if (R < 0 || N < 0 || C < 0) return 0;
@@ -1468,6 +1831,30 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
         FRCNN_LAUNCH_CHECK("roi_pool_fwd_bal_kernel");
         return FRCNN_OK;
     }
+    if (rois_sorted && (!var || is("px16") || is("px16S") || is("px16p") || is("px8q") || is("px8qS") ||
+                        is("px8qC"))) {
+        const PxPlan pl = px_plan(C, N, H, W, PH, PW, is("px8q") || is("px8qS") || is("px8qC") ? 8
+                                                      : (is("px16") || is("px16S") || is("px16p")) ? 16 : 0);
+        if (pl.cg) {
+            const int mode = (is("px16S") || is("px8qS")) ? 1 : is("px8qC") ? 2 : is("px16p") ? 3 : 0;
+            return px_launch(pl, mode, x, rois, R, C, H, W, PH, PW, spatial_scale, out, argmax, HeadArgs{}, st);
+        }
+    }
+    if (px8_ok && rois_sorted && (is("px8r") || is("px8rS"))) {
+        const size_t lds = 2 * HW * sizeof(float4);
+        int64_t sp = split8;
+        if (const char* s = getenv("FRCNN_ROIPOOL_SPLIT")) sp = std::atoi(s);
+        sp = sp < 1 ? 1 : (sp > 64 ? 64 : sp);
+        dim3 grid(C / 8, N + 1, static_cast<unsigned>(sp));
+        if (is("px8rS"))  // timing probe: no stores
+            hipLaunchKernelGGL((roi_pool_fwd_px8r_kernel<1024, 1>), grid, dim3(1024), lds, st, x, rois,
+                               static_cast<int>(R), C, H, W, PH, PW, spatial_scale, out, argmax);
+        else
+            hipLaunchKernelGGL((roi_pool_fwd_px8r_kernel<1024>), grid, dim3(1024), lds, st, x, rois,
+                               static_cast<int>(R), C, H, W, PH, PW, spatial_scale, out, argmax);
+        FRCNN_LAUNCH_CHECK("roi_pool_fwd_px8r_kernel");
+        return FRCNN_OK;
+    }
     if (px8_ok && rois_sorted && (is("px8sorted") || (kSortedDefault == 0 && !var))) {
         dim3 grid(C / 8, N + 1, static_cast<unsigned>(split8));
         hipLaunchKernelGGL((roi_pool_fwd_px8_kernel<1024, true>), grid, dim3(1024), 2 * tile_bytes, st,
@@ -1545,6 +1932,34 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
                            st, x, rois, N, C, H, W, PH, PW, spatial_scale, out, argmax);
     FRCNN_LAUNCH_CHECK("roi_pool_fwd_kernel");
     return FRCNN_OK;
+}
+
+extern "C" int frcnn_roi_pool_fwd_head(const float* x, const float* rois, const float* roi_inds,
+                                       int64_t R, int N, int C, int H, int W, int PH, int PW,
+                                       float img_h, float img_w, float spatial_scale,
+                                       int rois_sorted, float* boxes, float* out, int32_t* argmax,
+                                       void* workspace, size_t ws_bytes, void* stream) {
+    FRCNN_REQUIRE(R >= 0 && N >= 0 && C >= 0 && H >= 0 && W >= 0, "frcnn_roi_pool_fwd_head: bad shape");
+    FRCNN_REQUIRE(PH > 0 && PW > 0 && PH * PW <= kMaxBins,
+                  "frcnn_roi_pool_fwd_head: output_size must have 1..%d bins", kMaxBins);
+    FRCNN_REQUIRE(R <= 0x7fffffff && N <= 65534, "frcnn_roi_pool_fwd_head: too many rois / images");
+    if (R == 0) return FRCNN_OK;
+    FRCNN_REQUIRE(rois && roi_inds && boxes, "frcnn_roi_pool_fwd_head: null pointer");
+    const char* var = getenv("FRCNN_ROIPOOL_VARIANT");
+    const PxPlan pl = (rois_sorted && C > 0 && (!var || std::strcmp(var, "px8q") == 0 ||
+                                               std::strcmp(var, "px16") == 0))
+                          ? px_plan(C, N, H, W, PH, PW, !var ? 0 : (std::strcmp(var, "px8q") == 0 ? 8 : 16))
+                          : PxPlan{};
+    if (!pl.cg || reinterpret_cast<uintptr_t>(rois) % 16 != 0) {
+        int rc = frcnn_roi_transform(rois, roi_inds, R, img_h, img_w, H, W, boxes, stream);
+        if (rc != FRCNN_OK) return rc;
+        if (C == 0) return FRCNN_OK;
+        return frcnn_roi_pool_fwd(x, boxes, R, N, C, H, W, PH, PW, spatial_scale, rois_sorted, out,
+                                  argmax, workspace, ws_bytes, stream);
+    }
+    FRCNN_REQUIRE(x && out && argmax, "frcnn_roi_pool_fwd_head: null pointer");
+    const HeadArgs hd{roi_inds, img_h, img_w, static_cast<float>(H), static_cast<float>(W), boxes};
+    return px_launch(pl, 0, x, rois, R, C, H, W, PH, PW, spatial_scale, out, argmax, hd, as_stream(stream));
 }
 
 namespace {

@@ -1,10 +1,10 @@
 """Second-stage head (nets/heads.py) on the HIP path.
 
 ``ResnetHead.forward`` keeps the reference signature (nets/heads.py:27).  The
-RoI transform + ``[idx, box]`` pack (nets/heads.py:42-47) is one HIP kernel
-and RoIPool forward/backward (nets/heads.py:48) are the HIP kernels behind
-``ops.roi_pool``; the classifier (layer4 + avgpool) and the two FCs stay
-plain PyTorch (not the target).
+RoI transform + ``[idx, box]`` pack (nets/heads.py:42-47) and RoIPool forward
+(nets/heads.py:48) are one HIP launch (``ops.roi_pool_head``) when the RoIs
+are grouped by image, with roi_pool's HIP backward; the classifier (layer4 +
+avgpool) and the two FCs stay plain PyTorch (not the target).
 """
 from __future__ import annotations
 
@@ -27,16 +27,15 @@ class ResnetHead(nn.Module):
         """-> (cls [N, n_classes, n_sample], reg [N, n_sample, n_classes*4])."""
         N = x.shape[0]
         dev = _lib.device()
-        ri_in = torch.as_tensor(roi_inds).detach()
-        sorted_inds = None
-        if not ri_in.is_cuda:  # train.py builds roi_inds on the host, grouped by image
-            bi = ri_in.to(torch.int64)
-            sorted_inds = bool((bi[1:] >= bi[:-1]).all()) if bi.numel() > 1 else True
         r = torch.as_tensor(rois).detach().to(dev, torch.float32).contiguous()
-        ri = ri_in.to(dev, torch.float32).contiguous()
-        boxes = ops.roi_transform(r, ri, img_h, img_w, x.shape[2], x.shape[3])
-        cropped = ops.roi_pool(x, boxes, (self.roi_size, self.roi_size), self.spatial_scale,
-                               rois_sorted=sorted_inds)
+        ri = torch.as_tensor(roi_inds).detach().to(dev, torch.float32).contiguous()
+        # RPN.forward (nets/rpn.py:129-136) and train.py's sampler loop group the
+        # RoIs by image; the one-launch path relies on that, so check it.
+        bi = ri.to(torch.int32)
+        sorted_inds = bool((bi[1:] >= bi[:-1]).all()) if bi.numel() > 1 else True
+        out_dev = x.device
+        cropped = ops.roi_pool_head(x, r, ri, (self.roi_size, self.roi_size), img_h, img_w,
+                                    self.spatial_scale, rois_sorted=sorted_inds)[0].to(out_dev)
         fc6 = self.classifier(cropped)
         fc6 = fc6.view(fc6.shape[0], -1)
         reg = self.reg(fc6)

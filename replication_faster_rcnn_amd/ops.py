@@ -101,6 +101,55 @@ class _RoIPoolFunction(torch.autograd.Function):
         return gi, None, None, None, None, None
 
 
+class _RoIPoolHeadFunction(torch.autograd.Function):
+    """nets/heads.py:42-48 (RoI transform + pack + roi_pool) as one op; the
+    backward is roi_pool's, on the [R,5] boxes the forward wrote."""
+
+    @staticmethod
+    def forward(ctx, x, rois, roi_inds, ph, pw, img_h, img_w, ss, rois_sorted):
+        lib = _lib.load()
+        N, C, H, W = x.shape
+        R = rois.size(0)
+        boxes = torch.empty((R, 5), dtype=torch.float32, device=x.device)
+        out = torch.empty((R, C, ph, pw), dtype=torch.float32, device=x.device)
+        am = torch.empty((R, C, ph, pw), dtype=torch.int32, device=x.device)
+        ws = _lib.workspace(lib.frcnn_roi_pool_fwd_workspace_size(R, N, C), x.device)
+        _lib.check(lib.frcnn_roi_pool_fwd_head(
+            _lib.ptr(x), _lib.ptr(rois), _lib.ptr(roi_inds), R, N, C, H, W, ph, pw, float(img_h),
+            float(img_w), float(ss), int(bool(rois_sorted)), _lib.ptr(boxes), _lib.ptr(out),
+            _lib.ptr(am), _lib.ptr(ws), ws.numel(), _lib.stream_ptr()), "roi_pool_head forward")
+        ctx.save_for_backward(boxes, am)
+        ctx.meta = (tuple(x.shape), ss)
+        ctx.mark_non_differentiable(am, boxes)
+        return out, am, boxes
+
+    @staticmethod
+    def backward(ctx, grad_out, _grad_am, _grad_boxes):
+        boxes, am = ctx.saved_tensors
+        shape, ss = ctx.meta
+        gi = _roi_pool_bwd(grad_out.contiguous().float(), boxes, am, shape, ss)
+        return gi, None, None, None, None, None, None, None, None
+
+
+def roi_pool_head(input: torch.Tensor, rois: torch.Tensor, roi_inds: torch.Tensor, output_size,
+                  img_h, img_w, spatial_scale: float = 1.0, rois_sorted: bool = False):
+    """ResnetHead's RoI transform + ``[idx, box]`` pack + roi_pool
+    (nets/heads.py:42-48) in one call on device tensors: rois fp32 [R,4] in
+    image pixels, roi_inds [R] -> (out [R,C,ph,pw], argmax int32, boxes [R,5]).
+    ``rois_sorted`` promises RoIs grouped by non-decreasing image index (RPN
+    proposals, train.py's sample_rois): then the transform runs inside the
+    pool kernel."""
+    if input.dim() != 4:
+        raise RuntimeError("input must be [N, C, H, W]")
+    if rois.dim() != 2 or rois.size(1) != 4 or roi_inds.dim() != 1 or roi_inds.size(0) != rois.size(0):
+        raise RuntimeError(f"rois must be [R, 4] and roi_inds [R]; got {tuple(rois.shape)}, "
+                           f"{tuple(roi_inds.shape)}")
+    ph, pw = (output_size, output_size) if isinstance(output_size, int) else tuple(output_size)
+    x = _to_dev(input)
+    return _RoIPoolHeadFunction.apply(x.contiguous(), _to_dev(rois), _to_dev(roi_inds), int(ph), int(pw),
+                                      float(img_h), float(img_w), float(spatial_scale), bool(rois_sorted))
+
+
 def _boxes_to_rois(boxes: Union[torch.Tensor, List[torch.Tensor]]) -> torch.Tensor:
     if isinstance(boxes, (list, tuple)):  # torchvision's List[Tensor[L,4]] form
         parts = [torch.cat([torch.full((b.size(0), 1), i, dtype=b.dtype, device=b.device), b], 1)

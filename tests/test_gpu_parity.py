@@ -298,15 +298,22 @@ def _rand_rois(r, b, H, W, lo=-3, span=40):
     return np.concatenate([np.asarray(b, np.float32)[:, None], xy, xy + wh], 1).astype(np.float32)
 
 
-@pytest.mark.parametrize("variant", ["bal2", "bal"])
+@pytest.mark.parametrize("variant", ["bal2", "bal", "px8q@1", "px8q@3", "px8q@64", "px8r@1", "px8r@2", "px8r@5", "px16@1", "px16@3"])
 @pytest.mark.parametrize("case", ["many_images", "invalid_ends", "unsorted_promised_sorted",
                                   "single_roi", "gaps", "one_image_tiny_rois", "uniform_sizes",
                                   "ph5", "cfg4_shape"])
 def test_roi_pool_balanced_path(case, variant, monkeypatch):
     """The cost-balanced single-launch forward (default for RoIs grouped by
     image): segment boundaries, run lists (and their overflow / block-search
-    fallback), out-of-range batch indices, and any RoI order bit-exact."""
+    fallback), out-of-range batch indices, and any RoI order bit-exact.
+    px8q / px8r (strided per-image shares, `@k` = shares per image) need the
+    promised grouping, so it skips the unsorted case."""
+    variant, _, split = variant.partition("@")
+    if variant.startswith(("px8q", "px8r", "px16")) and case == "unsorted_promised_sorted":
+        pytest.skip("px8q requires RoIs grouped by image")
     monkeypatch.setenv("FRCNN_ROIPOOL_VARIANT", variant)
+    if split:
+        monkeypatch.setenv("FRCNN_ROIPOOL_SPLIT", split)
     r = np.random.default_rng(sum(map(ord, case)))
     ph = 5 if case == "ph5" else 7
     N, C, H, W = 4, 16, 20, 27
@@ -343,7 +350,7 @@ def test_roi_pool_balanced_path(case, variant, monkeypatch):
     assert (out.cpu().numpy()[~valid] == 0).all() and (am.cpu().numpy()[~valid] == -1).all()
 
 
-@pytest.mark.parametrize("variant", ["bal2", "bal2ns", "bal", "px8sorted"])
+@pytest.mark.parametrize("variant", ["px16", "px8r", "px8q", "bal2", "bal2ns", "bal", "px8sorted"])
 def test_roi_pool_sorted_variants_cfg2(variant, monkeypatch):
     """The two single-launch forwards for image-grouped RoIs at the bench shape
     (8 x 256 x 38 x 63, 300 proposals per image) agree bit for bit with the
@@ -362,7 +369,7 @@ def test_roi_pool_sorted_variants_cfg2(variant, monkeypatch):
     assert np.array_equal(out.cpu().numpy()[pick], oo)
 
 
-@pytest.mark.parametrize("variant", ["bal2", "bal2ns", "bal", "px8sorted"])
+@pytest.mark.parametrize("variant", ["px16", "px8r", "px8q", "bal2", "bal2ns", "bal", "px8sorted"])
 def test_roi_pool_sorted_special_values(variant, monkeypatch):
     """The image-grouped forwards on signed zeros, -FLT_MAX, +-inf and NaN
     windows, RoIs partly / fully outside the map (bal2: clamped revisits and
@@ -389,3 +396,51 @@ def test_roi_pool_sorted_special_values(variant, monkeypatch):
     oo, oa = orc.roi_pool_forward(x, rois, 7)
     assert np.array_equal(am.cpu().numpy(), oa)
     assert np.array_equal(out.cpu().numpy().view(np.uint32), oo.view(np.uint32))
+
+
+@pytest.mark.parametrize("case", ["grouped", "grouped_split3", "grouped_cg8", "ungrouped", "out_of_range",
+                                  "c_not8", "many_per_image"])
+def test_roi_pool_head_fused(case, monkeypatch):
+    """ops.roi_pool_head = nets/heads.py:42-48 (transform + pack + roi_pool) in
+    one call: boxes, out and argmax bit-exact vs the oracle's roi_transform +
+    roi_pool, and its gradient identical to roi_pool's on the same boxes."""
+    monkeypatch.delenv("FRCNN_ROIPOOL_VARIANT", raising=False)
+    if case == "grouped_split3":
+        monkeypatch.setenv("FRCNN_ROIPOOL_SPLIT", "3")
+    if case == "grouped_cg8":
+        monkeypatch.setenv("FRCNN_ROIPOOL_VARIANT", "px8q")
+    r = np.random.default_rng(sum(map(ord, case)))
+    N, C, H, W, img_h, img_w = 3, 16, 38, 63, 600.0, 1000.0
+    if case == "c_not8":
+        C = 12
+    R = 257
+    if case == "many_per_image":  # > geo_cap RoIs per workgroup: several geometry chunks
+        N, C, R = 1, 16, 3000
+        monkeypatch.setenv("FRCNN_ROIPOOL_SPLIT", "1")
+    inds = np.sort(r.integers(0, N, R)).astype(np.float32)
+    if case == "ungrouped":
+        r.shuffle(inds)
+    if case == "out_of_range":
+        inds[:3] = -1.0
+        inds[-4:] = N + 1
+        inds = np.sort(inds)
+    y1 = r.uniform(-20, img_h, R).astype(np.float32)
+    x1 = r.uniform(-20, img_w, R).astype(np.float32)
+    rois = np.stack([y1, x1, y1 + r.uniform(0, 400, R).astype(np.float32),
+                     x1 + r.uniform(0, 600, R).astype(np.float32)], 1).astype(np.float32)
+    x = r.standard_normal((N, C, H, W), dtype=np.float32)
+    x[:, :, 5:15, 5:25] = np.round(x[:, :, 5:15, 5:25])  # ties
+    xt = torch.from_numpy(x).to(DEV).requires_grad_(True)
+    out, am, boxes = ops.roi_pool_head(xt, torch.from_numpy(rois).to(DEV), torch.from_numpy(inds).to(DEV),
+                                       7, img_h, img_w, rois_sorted=case != "ungrouped")
+    oboxes = orc.roi_transform(rois, inds, img_h, img_w, H, W)
+    assert np.array_equal(boxes.cpu().numpy().view(np.uint32), oboxes.view(np.uint32))
+    oo, oa = orc.roi_pool_forward(x, oboxes, 7)
+    valid = (inds.astype(np.int64) >= 0) & (inds.astype(np.int64) < N)
+    assert np.array_equal(am.cpu().numpy()[valid], oa[valid])
+    assert np.array_equal(out.detach().cpu().numpy()[valid].view(np.uint32), oo[valid].view(np.uint32))
+    assert (out.detach().cpu().numpy()[~valid] == 0).all() and (am.cpu().numpy()[~valid] == -1).all()
+    g = torch.from_numpy(r.standard_normal(out.shape, dtype=np.float32)).to(DEV)
+    (out * g).sum().backward()
+    og = orc.roi_pool_backward(g.cpu().numpy(), oboxes, am.cpu().numpy(), x.shape)  # -1 rows skipped
+    assert np.array_equal(xt.grad.cpu().numpy(), og)

@@ -1,6 +1,8 @@
 """A/B timing of RoIPool forward variants on one device, interleaved rounds.
 
-    python tools/ab_roi_pool.py [--config cfg2] [--variants wave4,wave8,tile]
+    python tools/ab_roi_pool.py [--config cfg2] [--variants wave4,wave8,tile,px8q@4]
+
+`name@k` runs variant `name` with FRCNN_ROIPOOL_SPLIT=k (RoI shares per image).
 
 Inputs are the bench's: cfg features + the proposals of the batch.  Every
 variant's output is checked bit-equal to the first variant's.
@@ -42,8 +44,13 @@ def main():
     ref = None
     times = {v: [] for v in variants}
     for rnd in range(a.rounds):
-        for v in variants:
-            srt = v in ("sorted", "bal", "balcnt", "px8sorted", "balnc", "balns", "bal2", "bal2ns", "bal2c", "bal2b")  # single-launch paths (RoIs grouped by image)
+        for vs in variants:
+            v, _, sp = vs.partition("@")
+            if sp:
+                os.environ["FRCNN_ROIPOOL_SPLIT"] = sp
+            else:
+                os.environ.pop("FRCNN_ROIPOOL_SPLIT", None)
+            srt = v in ("px16p", "px16", "px16S", "px8r", "px8rS", "px8q", "px8qn", "px8qS", "px8qC", "sorted", "bal", "balcnt", "px8sorted", "balnc", "balns", "bal2", "bal2ns", "bal2c", "bal2b")  # single-launch paths (RoIs grouped by image)
             if v == "sorted":
                 os.environ.pop("FRCNN_ROIPOOL_VARIANT", None)
             else:
@@ -51,15 +58,15 @@ def main():
             out, am = ops._roi_pool_fwd(x, boxes, 7, 7, 1.0, srt)
             if ref is None:
                 ref = (out.clone(), am.clone())
-            elif rnd == 0 and v not in ("balnc", "balns", "bal2c", "bal2b"):
-                assert torch.equal(out, ref[0]) and torch.equal(am, ref[1]), f"variant {v} differs"
+            elif rnd == 0 and v not in ("px16S", "px8rS", "px8qS", "px8qC", "balnc", "balns", "bal2c", "bal2b"):
+                assert torch.equal(out, ref[0]) and torch.equal(am, ref[1]), f"variant {vs} differs"
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.iters):
                 ops._roi_pool_fwd(x, boxes, 7, 7, 1.0, srt)
             e1.record()
             torch.cuda.synchronize()
-            times[v].append(e0.elapsed_time(e1) / a.iters * 1e3)
+            times[vs].append(e0.elapsed_time(e1) / a.iters * 1e3)
     res = {v: {"us_median": float(np.median(t)), "us_min": float(np.min(t)),
                "GBps": alg / (np.median(t) * 1e-6) / 1e9} for v, t in times.items()}
     print(json.dumps({"config": a.config, "R": R, "alg_bytes": alg, "variants": res}, indent=1))

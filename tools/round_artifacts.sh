@@ -19,4 +19,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
     python3 bench.py --cpu-seconds 0 > "$OUT/prof_bench.json" 2>&1
 rc=$?; echo "rocprof rc=$rc"
 if [ $rc -ne 0 ]; then exit $rc; fi
-bash tools/pmc_roi_pool.sh "$OUT/pmc" sorted cfg2
+bash tools/pmc_roi_pool.sh "$OUT/pmc" bench cfg2 && \
+    python3 tools/summarize_pmc.py "$OUT/pmc" px8q_kernel --config cfg2 > "$OUT/pmc_summary.txt" && cat "$OUT/pmc_summary.txt"
