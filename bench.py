@@ -9,6 +9,11 @@ input already resident in HBM (BASELINE.json configs[1] = cfg2: 8 images of
     propose (decode+clamp+filter+top-k+NMS+post, anchors generated in-kernel)
     -> RoI transform + pack + RoIPool forward (nets/heads.py:42-48, one launch)
 
+By default the proposal layer and the RoIPool run on two HIP streams, so step
+k+1's proposals (8 one-image workgroups + two small chip-wide kernels) run
+beside step k's RoIPool (every step still does all of its work; --streams 1
+serialises them).
+
 For N>1 (torch.distributed.run, one process per GPU) every rank runs its own
 batch of 8 images (weak scaling, images seeded by global index) and the
 padded detections are all-gathered over RCCL at the end of each step -- the
@@ -39,6 +44,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--streams", type=int, default=2, choices=(1, 2),
+                    help="2: the proposal layer of step k+1 runs on its own HIP stream beside "
+                         "step k's RoIPool (each step still does all of its work)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-baseline sample (rank 0, N=1 only); 0 disables")
     return ap.parse_args()
@@ -119,21 +127,32 @@ def main():
     inds = torch.arange(N, device=dev, dtype=torch.float32).repeat_interleave(post)
     ev = []
 
+    # streams=2: two HIP streams, step k+1's proposals beside step k's RoIPool
+    # (stream priorities measured: no effect)
+    s_prop = torch.cuda.current_stream() if args.streams == 1 else torch.cuda.Stream()
+    s_pool = torch.cuda.current_stream() if args.streams == 1 else torch.cuda.Stream()
+
     def step(timed):
-        rois, idx, cnt = ops.propose(sc, de, img_w=c["img_w"], img_h=c["img_h"],
-                                     pre_nms=c["pre_nms"], post_nms=post, anchor_base=base,
-                                     feat_h=c["feat_h"], feat_w=c["feat_w"])
-        if timed:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-        # ResnetHead's transform + pack + roi_pool (nets/heads.py:42-48): one launch
-        pooled, am, boxes = ops.roi_pool_head(x, rois.view(-1, 4), inds, 7, c["img_h"], c["img_w"],
-                                              rois_sorted=True)
-        if timed:
-            e1.record()
-            ev.append((e0, e1))
-        if world > 1:  # the only collective: detections of all ranks (RCCL over xGMI)
-            fdist.all_gather_detections(rois, idx, cnt)
+        with torch.cuda.stream(s_prop):
+            rois, idx, cnt = ops.propose(sc, de, img_w=c["img_w"], img_h=c["img_h"],
+                                         pre_nms=c["pre_nms"], post_nms=post, anchor_base=base,
+                                         feat_h=c["feat_h"], feat_w=c["feat_w"])
+            if world > 1:  # the only collective: detections of all ranks (RCCL over xGMI)
+                fdist.all_gather_detections(rois, idx, cnt)
+            ready = torch.cuda.Event()
+            ready.record(s_prop)
+        with torch.cuda.stream(s_pool):
+            s_pool.wait_event(ready)
+            rois.record_stream(s_pool)  # allocated on s_prop, read on s_pool
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s_pool)
+            # ResnetHead's transform + pack + roi_pool (nets/heads.py:42-48): one launch
+            pooled, am, boxes = ops.roi_pool_head(x, rois.view(-1, 4), inds, 7, c["img_h"], c["img_w"],
+                                                  rois_sorted=True)
+            if timed:
+                e1.record(s_pool)
+                ev.append((e0, e1))
         return cnt
 
     for _ in range(args.warmup):
@@ -171,7 +190,8 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
         "config": {"workload": f"{args.config}: {N} VOC-shape images/GPU 600x1000, 38x63x9 anchors, "
                                f"{c['pre_nms']}->{post} NMS@0.7, RoIPool 7x7x{C}",
-                   "global_batch": world * N, "parallelism": f"dp{world} (per-image sharding)"},
+                   "global_batch": world * N, "parallelism": f"dp{world} (per-image sharding)",
+                   "streams": args.streams},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "roi_pool_fwd_px8q_kernel<head>", "kernel_us": roi_ms * 1e3,
