@@ -128,7 +128,9 @@ def main():
     ev = []
 
     # streams=2: two HIP streams, step k+1's proposals beside step k's RoIPool
-    # (stream priorities measured: no effect)
+    # (measured: stream priorities change nothing; holding step k+1's proposals
+    # until step k's pool is issued gives the pool the whole chip, 68 vs 75 us,
+    # but costs 17 % of the throughput)
     s_prop = torch.cuda.current_stream() if args.streams == 1 else torch.cuda.Stream()
     s_pool = torch.cuda.current_stream() if args.streams == 1 else torch.cuda.Stream()
 
