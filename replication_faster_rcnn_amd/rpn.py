@@ -106,6 +106,8 @@ class RPN(nn.Module):
             pre_nms=pl.pre_nms, post_nms=pl.post_nms, nms_thresh=pl.nms_threshold,
             min_size=pl.min_size, anchor_base=self._base_dev, feat_h=conv_h, feat_w=conv_w,
             feat_stride=self.feat_stride)
+        # padded per-image form (the batched samplers take it as is) + fg scores
+        self.rois_padded, self.rois_count, self.fg_scores = rois_p, cnt, cls_fg_softmax.detach()
         counts = cnt.tolist()  # the one host sync: the output length is data-dependent
         rois = torch.cat([rois_p[i, :c] for i, c in enumerate(counts)], 0).to(x.device)
         roi_inds = torch.cat([torch.full((c,), float(i)) for i, c in enumerate(counts)], 0)

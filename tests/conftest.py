@@ -25,3 +25,12 @@ def golden():
         return cache[name]
 
     return load
+
+
+@pytest.fixture
+def rng_guard():
+    """Restore numpy's global RNG (the samplers consume it like the reference)."""
+    import numpy as np
+    st = np.random.get_state()
+    yield
+    np.random.set_state(st)

@@ -22,13 +22,6 @@ def sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-@pytest.fixture
-def rng_guard():
-    st = np.random.get_state()
-    yield
-    np.random.set_state(st)
-
-
 def test_bbox_iou_known_answer(golden):
     g = golden("anchors.npz")
     out = U.bbox_iou(g["iou_main_a"], g["iou_main_b"])
