@@ -112,21 +112,54 @@ def cpu_baseline(cfg, seconds):
                       f"nms/roi_pool), after 1 warm-up image; {el:.1f} s on {os.cpu_count()}-cpu host"}
 
 
-def main():
-    args = parse()
-    world, rank, local = setup_dist(args.gpus)
-    dev = torch.device("cuda", local)
-    from replication_faster_rcnn_amd import anchors as A, ops
+def cpu_baseline_train(cfg, seconds):
+    """Oracle CPU training-step path per image (train.py:67-108 loops + the
+    RoIPool forward/backward of nets/heads.py:48), bounded sample."""
+    from oracle import ref_numpy as orc
+    from replication_faster_rcnn_amd import synth
+    c = synth.CONFIGS[cfg]
+    base = orc.generate_anchor_base(anchor_scales=c["scales"])
+    anchors = orc.generate_anchors(base, 16, c["feat_w"], c["feat_h"])
+    A = len(anchors)
+    g = np.random.default_rng(1).standard_normal((128, c["C"], 7, 7), dtype=np.float32)
+    np.random.seed(0)
+    done, t0, i, warm = 0, time.perf_counter(), 0, True
+    while True:
+        sc, de = synth.rpn_scores(A, 0, i), synth.rpn_deltas(A, 0, i)
+        x = synth.features(c["C"], c["feat_h"], c["feat_w"], 0, i)[None]
+        bx, lb = synth.gt_boxes(c["img_h"], c["img_w"], 32, 0, i)
+        v = lb != -1
+        ts = time.perf_counter()
+        rois, _ = orc.propose_one(anchors, sc, de, c["img_w"], c["img_h"], c["pre_nms"], c["post_nms"])
+        orc.anchor_target(bx[v], anchors)
+        s_roi = orc.proposal_target(rois, bx[v], lb[v])[0]
+        boxes = orc.roi_transform(s_roi.astype(np.float32), np.zeros(len(s_roi), np.float32),
+                                  c["img_h"], c["img_w"], c["feat_h"], c["feat_w"])
+        _, am = orc.roi_pool_forward(x, boxes, 7, 1.0)
+        orc.roi_pool_backward(g[:len(boxes)], boxes, am, x.shape)
+        te = time.perf_counter()
+        if warm:
+            warm, t0 = False, te
+            continue
+        done += 1
+        i += 1
+        if te - t0 >= seconds:
+            break
+    el = time.perf_counter() - t0
+    return {"value": done / el, "unit": "images/sec", "cores": 1, "kind": "port",
+            "sample": f"{done} {cfg}-shaped training images, one at a time (oracle: numpy targets with "
+                      f"the global MT19937 + 1-thread C nms/roi_pool fwd+bwd), after 1 warm-up image; "
+                      f"{el:.1f} s on {os.cpu_count()}-cpu host"}
+
+
+def inference_step_fn(args, c, sc, de, x, base, world, ev):
+    """cfg1-4: propose -> (RCCL all-gather of detections) -> RoI transform +
+    pack + RoIPool forward (nets/rpn.py:102-138, nets/heads.py:42-48)."""
+    from replication_faster_rcnn_amd import ops
     from replication_faster_rcnn_amd import dist as fdist
-    per_rank = c_batch(args.config)
-    mine = fdist.shard(per_rank * world, rank, world)  # weak scaling: per_rank images per GPU
-    c, sc, de, x = make_inputs(args.config, len(mine), mine.start, dev)
-    N = sc.size(0)
-    base = A.generate_anchor_base_device(anchor_scales=c["scales"])
+    N, dev = sc.size(0), sc.device
     post = c["post_nms"]
     inds = torch.arange(N, device=dev, dtype=torch.float32).repeat_interleave(post)
-    ev = []
-
     # streams=2: two HIP streams, step k+1's proposals beside step k's RoIPool
     # (measured: stream priorities change nothing; holding step k+1's proposals
     # until step k's pool is issued gives the pool the whole chip, 68 vs 75 us,
@@ -154,8 +187,85 @@ def main():
                                                   rois_sorted=True)
             if timed:
                 e1.record(s_pool)
-                ev.append((e0, e1))
+                ev["fwd"].append((e0, e1))
         return cnt
+    return step
+
+
+def train_step_fn(args, c, sc, de, x, base, world, ev, first_image):
+    """cfg5 (training step, train.py:59-127 minus the dense layers): propose
+    (12000->600) -> anchor targets of every image -> proposal targets of every
+    image (numpy's MT19937 stream kept on the device, sync-free, in the
+    reference's order: all AT, then all PT) -> sampled RoIs fp64->fp32 ->
+    RoI transform + pack + RoIPool forward -> RoIPool backward of a resident
+    upstream gradient (the head's dL/dpool)."""
+    from replication_faster_rcnn_amd import anchors as A, ops, synth, targets
+    from replication_faster_rcnn_amd.utils import rng_state_to_device
+    N, dev = sc.size(0), sc.device
+    S = 128
+    anchors = A.generate_anchors(base, 16, c["feat_w"], c["feat_h"]).to(dev)
+    gl = [synth.gt_boxes(c["img_h"], c["img_w"], 32, 0, first_image + i) for i in range(N)]
+    boxes = torch.from_numpy(np.stack([b for b, _ in gl])).to(dev)
+    labels = torch.from_numpy(np.stack([l for _, l in gl])).to(dev)
+    np.random.seed(0)
+    rng, _ = rng_state_to_device(dev)
+    inds = torch.arange(N, device=dev, dtype=torch.float32).repeat_interleave(S)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1)
+    grad = torch.randn((N * S, x.size(1), 7, 7), device=dev, generator=gen)
+    s_prop = torch.cuda.current_stream() if args.streams == 1 else torch.cuda.Stream()
+    s_pool = torch.cuda.current_stream() if args.streams == 1 else torch.cuda.Stream()
+    state = {}
+
+    def step(timed):
+        with torch.cuda.stream(s_prop):
+            rois, _, cnt = ops.propose(sc, de, img_w=c["img_w"], img_h=c["img_h"],
+                                       pre_nms=c["pre_nms"], post_nms=c["post_nms"],
+                                       anchor_base=base, feat_h=c["feat_h"], feat_w=c["feat_w"])
+            reg_t, lab = targets.anchor_targets(boxes, labels, anchors, rng=rng)
+            s_roi, s_reg, s_lab, s_cnt = targets.proposal_targets(rois, cnt, boxes, labels,
+                                                                  n_sample=S, rng=rng)
+            sample_rois = s_roi.float().view(-1, 4)          # train.py:86,102,107
+            ready = torch.cuda.Event()
+            ready.record(s_prop)
+        with torch.cuda.stream(s_pool):
+            s_pool.wait_event(ready)
+            sample_rois.record_stream(s_pool)
+            if timed:
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                e[0].record(s_pool)
+            pooled, am, bx = ops.roi_pool_head(x, sample_rois, inds, 7, c["img_h"], c["img_w"],
+                                               rois_sorted=True)
+            if timed:
+                e[1].record(s_pool)
+            gi = ops._roi_pool_bwd(grad, bx, am, tuple(x.shape), 1.0)
+            if timed:
+                e[2].record(s_pool)
+                ev["fwd"].append((e[0], e[1]))
+                ev["bwd"].append((e[1], e[2]))
+        state.update(s_cnt=s_cnt, lab=lab, gi=gi)
+        return s_cnt
+    step.state = state
+    return step
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args.gpus)
+    dev = torch.device("cuda", local)
+    from replication_faster_rcnn_amd import anchors as A
+    from replication_faster_rcnn_amd import dist as fdist
+    train = args.config == "cfg5"
+    per_rank = c_batch(args.config)
+    mine = fdist.shard(per_rank * world, rank, world)  # weak scaling: per_rank images per GPU
+    c, sc, de, x = make_inputs(args.config, len(mine), mine.start, dev)
+    N = sc.size(0)
+    base = A.generate_anchor_base_device(anchor_scales=c["scales"])
+    ev = {"fwd": [], "bwd": []}
+    if train:
+        step = train_step_fn(args, c, sc, de, x, base, world, ev, mine.start)
+    else:
+        step = inference_step_fn(args, c, sc, de, x, base, world, ev)
 
     for _ in range(args.warmup):
         cnt = step(False)
@@ -175,33 +285,49 @@ def main():
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    roi_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     R = int(cnt.sum().item())
+    if train and R != N * 128:  # train.py:102 assumes exactly 128 samples per image
+        raise RuntimeError(f"proposal targets: {cnt.tolist()} samples per image, expected 128")
     C, H, W = x.shape[1:]
     alg_bytes = N * C * H * W * 4 + R * 20 + 2 * R * C * 49 * 4
-    achieved = alg_bytes / (roi_ms * 1e-3) / 1e9
+    fwd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev["fwd"]]))
+    # the dominant kernel: RoIPool fwd (inference), RoIPool bwd (training step;
+    # same algorithmic bytes: grad + argmax read, rois, grad_in written)
+    dom_ms = float(np.mean([a.elapsed_time(b) for a, b in ev["bwd"]])) if train else fwd_ms
+    achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None
-    tpath = os.path.join(ROOT, "profiles", "roi_pool_fwd_traffic.json")
+    tpath = os.path.join(ROOT, "profiles", "roi_pool_bwd_traffic.json" if train
+                         else "roi_pool_fwd_traffic.json")
     if os.path.exists(tpath):
         traffic = json.load(open(tpath)).get(args.config, {}).get("hbm_bytes_per_launch")
     images = world * N * args.steps
+    if train:
+        workload = (f"{args.config}: training step, {N} images/GPU {c['img_h']}x{c['img_w']}, "
+                    f"{c['feat_h']}x{c['feat_w']}x9 anchors, {c['pre_nms']}->{c['post_nms']} NMS@0.7, "
+                    f"anchor targets vs 32 gt + proposal targets (128/img), RoIPool 7x7x{C} fwd+bwd")
+    else:
+        workload = (f"{args.config}: {N} VOC-shape images/GPU {c['img_h']}x{c['img_w']}, "
+                    f"{c['feat_h']}x{c['feat_w']}x{3 * len(c['scales'])} anchors, "
+                    f"{c['pre_nms']}->{c['post_nms']} NMS@0.7, RoIPool 7x7x{C}")
     rec = {
         "metric": "images/sec through RPN proposal+NMS+RoIPool; RoIPool HBM GB/s vs peak",
         "value": images / el, "unit": "images/sec", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-        "config": {"workload": f"{args.config}: {N} VOC-shape images/GPU 600x1000, 38x63x9 anchors, "
-                               f"{c['pre_nms']}->{post} NMS@0.7, RoIPool 7x7x{C}",
-                   "global_batch": world * N, "parallelism": f"dp{world} (per-image sharding)",
-                   "streams": args.streams},
+        "config": {"workload": workload, "global_batch": world * N,
+                   "parallelism": f"dp{world} (per-image sharding)", "streams": args.streams},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "roi_pool_fwd_px8q_kernel<head>", "kernel_us": roi_ms * 1e3,
-                     "alg_bytes_per_launch": alg_bytes},
+                     "kernel": "roi_pool_bwd_kernel" if train else "roi_pool_fwd_px8q_kernel<head>",
+                     "kernel_us": dom_ms * 1e3, "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": None,
     }
+    if train:
+        rec["roofline"]["fwd_us"] = fwd_ms * 1e3
+        rec["roofline"]["fwd_frac"] = alg_bytes / (fwd_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        rec["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
+        cb = cpu_baseline_train if train else cpu_baseline
+        rec["cpu_baseline"] = cb(args.config, args.cpu_seconds)
         rec["cpu_baseline"]["gpu_over_cpu"] = rec["value"] / rec["cpu_baseline"]["value"]
     if rank == 0:
         print(json.dumps(rec), flush=True)

@@ -1575,6 +1575,139 @@ __global__ void roi_pool_bwd_kernel(const float* __restrict__ grad,
     }
 }
 
+// Same plane-owner backward for PH*PW <= 64 (one bin per lane, the 7x7 head),
+// latency-hidden: a wave used to issue RoI t+1's argmax / grad / overlap-mask
+// loads only after RoI t's LDS adds had retired, so every RoI paid a full HBM
+// round trip (128 RoIs x ~2 us = the whole 288 us kernel at cfg5).  Here the
+// loads of RoI t+D are issued before RoI t is applied (a D-deep register ring,
+// slot index static after unrolling), and the RoI indices come from a 64-wide
+// VGPR window read with v_readlane, so no vector load sits between the ring's
+// loads in the in-order vmcnt queue.  Summation order per pixel is unchanged
+// (RoIs ascending, bins ascending within a RoI): bit-identical results.
+template <int D>
+__global__ __launch_bounds__(1024) void roi_pool_bwd_pf_kernel(
+    const float* __restrict__ grad, const int32_t* __restrict__ argmax,
+    const uint64_t* __restrict__ cmask, const int* __restrict__ list, const int* __restrict__ cnt,
+    int R, int C, int HW, int PHW, int PW, int CPW, float* __restrict__ grad_in) {
+    extern __shared__ __attribute__((aligned(16))) float planes[];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int b = blockIdx.y;
+    const int c = blockIdx.x * CPW + wid;
+    if (c >= C) return;  // whole wave; no workgroup barrier below
+    float* gplane = grad_in + (static_cast<size_t>(b) * C + c) * HW;
+    float* plane = planes + static_cast<size_t>(wid) * HW;
+    for (int i = lane; i < HW; i += 64) plane[i] = 0.0f;
+    const int nr = cnt[b];
+    // Grid neighbours that come earlier in bin order: left, up-left, up,
+    // up-right.  When every overlap of a RoI is among them (bins >= 1 pixel:
+    // windows only share their floor/ceil border row / column), a bin's rank
+    // among the bins with the same argmax pixel takes four fixed-lane reads
+    // instead of a walk over its overlap mask.
+    const int pw_i = lane % PW;
+    const bool has_l = pw_i > 0, has_u = lane >= PW;
+    const bool has_r = pw_i < PW - 1;
+    const int n_l = has_l ? lane - 1 : lane, n_u = has_u ? lane - PW : lane;
+    const int n_ul = (has_u && has_l) ? lane - PW - 1 : lane;
+    const int n_ur = (has_u && has_r) ? lane - PW + 1 : lane;
+    const uint64_t b_l = has_l ? 1ull << n_l : 0ull, b_u = has_u ? 1ull << n_u : 0ull;
+    const uint64_t b_ul = (has_u && has_l) ? 1ull << n_ul : 0ull;
+    const uint64_t b_ur = (has_u && has_r) ? 1ull << n_ur : 0ull;
+    const uint64_t nb_mask = b_l | b_u | b_ul | b_ur;
+    if (nr > 0) {
+        const int* lst = list + static_cast<size_t>(b) * R;  // wave-uniform: scalar loads
+        const bool act = lane < PHW;
+        // Loads are unconditional (idle lanes re-read bin 0, RoIs past the end
+        // re-read the last one): a conditional load makes the compiler wait
+        // for the whole vmcnt queue at the branch join, which undoes the ring.
+        const int kl = act ? lane : 0;
+        int am_r[D];
+        float g_r[D];
+        uint64_t cm_r[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int n = lst[d < nr ? d : nr - 1];
+            const size_t base = (static_cast<size_t>(n) * C + c) * PHW;
+            am_r[d] = argmax[base + kl];
+            g_r[d] = grad[base + kl];
+            cm_r[d] = cmask[static_cast<size_t>(n) * PHW + kl];
+            // keep the loop's issue order (slot by slot): the waitcnt pass then
+            // merges identical queues at the loop header instead of draining
+            asm volatile("" ::: "memory");
+        }
+        for (int t0 = 0; t0 < nr; t0 += D) {
+            // RoI indices of this group's refills (scalar loads: lgkmcnt, not
+            // in the vector-load queue)
+            int nx[D];
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const int tn = t0 + D + d;
+                nx[d] = lst[tn < nr ? tn : nr - 1];
+            }
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                // no early exit for the tail: a break would give the loop a
+                // second path into its header with another load order, and the
+                // waitcnt pass would drain the queue there every group
+                const bool live = t0 + d < nr;
+                // Take slot d's values into fresh registers (asm copies the
+                // compiler cannot coalesce away) so the refill lands in the
+                // slot's own registers: no back-edge copy, no wait on it.
+                int am;
+                float g;
+                uint32_t cm_lo, cm_hi;
+                asm volatile("v_mov_b32 %0, %1" : "=v"(am) : "v"(am_r[d]));
+                asm volatile("v_mov_b32 %0, %1" : "=v"(g) : "v"(g_r[d]));
+                asm volatile("v_mov_b32 %0, %1" : "=v"(cm_lo) : "v"(static_cast<uint32_t>(cm_r[d])));
+                asm volatile("v_mov_b32 %0, %1" : "=v"(cm_hi) : "v"(static_cast<uint32_t>(cm_r[d] >> 32)));
+                if (!live || !act) am = -1;
+                uint64_t pend = (act && am != -1) ? ((static_cast<uint64_t>(cm_hi) << 32) | cm_lo) : 0ull;
+                {  // refill this slot with RoI t + D before applying RoI t
+                    const int n = nx[d];
+                    const size_t base = (static_cast<size_t>(n) * C + c) * PHW;
+                    am_r[d] = argmax[base + kl];
+                    g_r[d] = grad[base + kl];
+                    cm_r[d] = cmask[static_cast<size_t>(n) * PHW + kl];
+                }
+                // depth = rank of this bin among the RoI's bins with the same
+                // argmax pixel (those windows all contain the pixel, so they
+                // overlap: candidates are the bits of the overlap mask)
+                int depth = 0;
+                if (__ballot((pend & ~nb_mask) != 0) == 0) {
+                    const int a_l = __builtin_amdgcn_ds_bpermute(n_l << 2, am);
+                    const int a_u = __builtin_amdgcn_ds_bpermute(n_u << 2, am);
+                    const int a_ul = __builtin_amdgcn_ds_bpermute(n_ul << 2, am);
+                    const int a_ur = __builtin_amdgcn_ds_bpermute(n_ur << 2, am);
+                    depth = ((pend & b_l) && a_l == am) + ((pend & b_u) && a_u == am) +
+                            ((pend & b_ul) && a_ul == am) + ((pend & b_ur) && a_ur == am);
+                } else {
+                    while (__ballot(pend != 0)) {
+                        const int p = pend ? __ffsll(static_cast<unsigned long long>(pend)) - 1 : lane;
+                        pend &= pend - 1;
+                        const int amp = __builtin_amdgcn_ds_bpermute(p << 2, am);
+                        if (p != lane && amp == am) ++depth;
+                    }
+                }
+                // apply in rank order; ranks are unique per pixel, so each
+                // round's read-add-write touches distinct pixels
+                for (int r = 0;; ++r) {
+                    if (am != -1 && depth == r) plane[am] += g;
+                    // round boundary: this round's LDS adds land before the
+                    // next round's reads of the same pixel (also a compiler barrier)
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (__ballot(am != -1 && depth > r) == 0) break;
+                }
+            }
+        }
+    }
+    if ((HW & 3) == 0) {
+        const float4* s4 = reinterpret_cast<const float4*>(plane);
+        float4* d4 = reinterpret_cast<float4*>(gplane);
+        for (int i = lane; i < HW / 4; i += 64) d4[i] = s4[i];
+    } else {
+        for (int i = lane; i < HW; i += 64) gplane[i] = plane[i];
+    }
+}
+
 // Outputs of RoIs with an out-of-range batch index: 0 / -1 (torchvision: UB).
 __global__ __launch_bounds__(256) void roi_pool_invalid_fill_kernel(const int* __restrict__ list,
                                                                     const int* __restrict__ cnt,
@@ -1979,6 +2112,12 @@ BwdWs carve_bwd(void* ws, int64_t R, int N, int PH, int PW) {
     return w;
 }
 constexpr size_t kPlaneBudget = 64 * 1024;  // LDS per workgroup for planes
+constexpr int kBwdRing = 8;                  // RoIs in flight per wave (pf kernel)
+// A/B switch for tools (FRCNN_BWD_VARIANT=plain: the unpipelined kernel)
+bool bwd_variant_is(const char* v) {
+    const char* e = std::getenv("FRCNN_BWD_VARIANT");
+    return e && std::strcmp(e, v) == 0;
+}
 }  // namespace
 
 extern "C" size_t frcnn_roi_pool_bwd_workspace_size(int64_t R, int N, int PH, int PW) {
@@ -2020,9 +2159,14 @@ extern "C" int frcnn_roi_pool_bwd(const float* grad, const float* rois, const in
         cpw = cpw > 16 ? 16 : cpw;
         cpw = cpw > C ? C : cpw;
         dim3 grid((C + cpw - 1) / cpw, N);
-        hipLaunchKernelGGL(roi_pool_bwd_kernel<true>, grid, dim3(64 * cpw), cpw * plane_bytes, st,
-                           grad, argmax, w.cmask, w.list, w.cnt, static_cast<int>(R), C,
-                           static_cast<int>(HW), PHW, cpw, grad_in);
+        if (PHW <= 64 && !bwd_variant_is("plain"))
+            hipLaunchKernelGGL(roi_pool_bwd_pf_kernel<kBwdRing>, grid, dim3(64 * cpw),
+                               cpw * plane_bytes, st, grad, argmax, w.cmask, w.list, w.cnt,
+                               static_cast<int>(R), C, static_cast<int>(HW), PHW, PW, cpw, grad_in);
+        else
+            hipLaunchKernelGGL(roi_pool_bwd_kernel<true>, grid, dim3(64 * cpw), cpw * plane_bytes, st,
+                               grad, argmax, w.cmask, w.list, w.cnt, static_cast<int>(R), C,
+                               static_cast<int>(HW), PHW, cpw, grad_in);
     } else {
         const int cpw = 4;
         dim3 grid((C + cpw - 1) / cpw, N);

@@ -5,7 +5,9 @@ per-image Python loops).
 = ProposalTargetCreator over all images.  Both consume numpy's GLOBAL legacy
 RNG exactly like the reference's per-image loops do (all images in order),
 by shipping the MT19937 state to the device and back (one round trip per
-call -- the only host synchronisation).
+call -- the only host synchronisation).  A caller that owns a device-resident
+RNG stream (``rng=``: int32 [625] from ``utils.rng_state_to_device``) skips the
+round trip: the state advances in place on the device, sync-free.
 """
 from __future__ import annotations
 
@@ -27,7 +29,7 @@ def _gt(boxes, labels, dev):
 
 
 def anchor_targets(boxes, labels, anchors, n_sample=256, pos_iou_thresh=0.7, neg_iou_thresh=0.3,
-                   pos_ratio=0.5, sample=True, internals=False):
+                   pos_ratio=0.5, sample=True, internals=False, rng=None):
     """boxes [N,G,4] fp64 (label -1 rows = padding), labels [N,G], anchors [A,4]
     -> reg fp64 [N,A,4], label int32 [N,A] (device tensors)."""
     lib = _lib.load()
@@ -42,13 +44,17 @@ def anchor_targets(boxes, labels, anchors, n_sample=256, pos_iou_thresh=0.7, neg
     am = torch.empty((N, A), dtype=torch.int32, device=dev) if internals else None
     mx = torch.empty((N, A), dtype=torch.float64, device=dev) if internals else None
     ws = _lib.workspace(lib.frcnn_anchor_target_workspace_size(N, A, G), dev)
-    rng, st = rng_state_to_device(dev) if sample else (None, None)
+    own = rng is None
+    if own:
+        rng, st = rng_state_to_device(dev) if sample else (None, None)
+    elif not sample:
+        rng = None
     _lib.check(lib.frcnn_anchor_target(N, A, G, _lib.ptr(a), _lib.ptr(b), _lib.ptr(l), int(n_sample),
                                        float(pos_iou_thresh), float(neg_iou_thresh),
                                        float(pos_ratio), _lib.ptr(rng), _lib.ptr(reg),
                                        _lib.ptr(lab), _lib.ptr(am), _lib.ptr(mx), _lib.ptr(ws),
                                        ws.numel(), _lib.stream_ptr()), "anchor_target")
-    if sample:
+    if sample and own:
         rng_state_from_device(rng, st)
     if internals:
         return reg, lab, am, mx
@@ -57,7 +63,8 @@ def anchor_targets(boxes, labels, anchors, n_sample=256, pos_iou_thresh=0.7, neg
 
 def proposal_targets(rois, rcount, boxes, labels, n_sample=128, pos_ratio=0.5, pos_iou_thresh=0.5,
                      neg_iou_thresh_high=0.5, neg_iou_thresh_low=0.0,
-                     reg_normalize_mean=(0., 0., 0., 0.), reg_normalize_std=(0.1, 0.1, 0.2, 0.2)):
+                     reg_normalize_mean=(0., 0., 0., 0.), reg_normalize_std=(0.1, 0.1, 0.2, 0.2),
+                     rng=None):
     """rois fp32 [N,Rp,4] + rcount int32 [N] -> (sample_roi fp64 [N,S,4],
     gt_roi_reg fp64 [N,S,4], gt_roi_label fp64 [N,S], count int32 [N])."""
     lib = _lib.load()
@@ -75,7 +82,9 @@ def proposal_targets(rois, rcount, boxes, labels, n_sample=128, pos_ratio=0.5, p
     mean = np.asarray(reg_normalize_mean, np.float32).astype(np.float64)
     std = np.asarray(reg_normalize_std, np.float32).astype(np.float64)
     ws = _lib.workspace(lib.frcnn_proposal_target_workspace_size(N, Rp, G, n_sample), dev)
-    rng, st = rng_state_to_device(dev)
+    own = rng is None
+    if own:
+        rng, st = rng_state_to_device(dev)
     _lib.check(lib.frcnn_proposal_target(N, Rp, _lib.ptr(r), _lib.ptr(c), G, _lib.ptr(b), _lib.ptr(l),
                                          int(n_sample), float(pos_ratio), float(pos_iou_thresh),
                                          float(neg_iou_thresh_high), float(neg_iou_thresh_low),
@@ -83,5 +92,6 @@ def proposal_targets(rois, rcount, boxes, labels, n_sample=128, pos_ratio=0.5, p
                                          _lib.ptr(s_roi), _lib.ptr(s_reg), _lib.ptr(s_lab),
                                          _lib.ptr(s_cnt), _lib.ptr(ws), ws.numel(),
                                          _lib.stream_ptr()), "proposal_target")
-    rng_state_from_device(rng, st)
+    if own:
+        rng_state_from_device(rng, st)
     return s_roi, s_reg, s_lab, s_cnt

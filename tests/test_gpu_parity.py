@@ -159,7 +159,9 @@ def test_roi_pool_golden(golden):
 
 
 @pytest.mark.parametrize("N,C,H,W,R,ph", [(8, 256, 38, 63, 2400, 7), (2, 3, 9, 11, 77, 3),
-                                          (1, 5, 4, 4, 40, 7), (2, 64, 50, 84, 300, 7)])
+                                          (1, 5, 4, 4, 40, 7), (2, 64, 50, 84, 300, 7),
+                                          (16, 24, 38, 38, 2048, 7), (5, 4, 12, 12, 3, 7),
+                                          (3, 8, 16, 16, 21, 8)])
 def test_roi_pool_vs_oracle(N, C, H, W, R, ph):
     r = np.random.default_rng(R)
     x = r.standard_normal((N, C, H, W), dtype=np.float32)
@@ -444,3 +446,30 @@ def test_roi_pool_head_fused(case, monkeypatch):
     (out * g).sum().backward()
     og = orc.roi_pool_backward(g.cpu().numpy(), oboxes, am.cpu().numpy(), x.shape)  # -1 rows skipped
     assert np.array_equal(xt.grad.cpu().numpy(), og)
+
+
+def test_roi_pool_bwd_ring_equals_plain(monkeypatch):
+    """The latency-hidden backward (8-RoI load ring) and the plain plane-owner
+    kernel give identical bits, incl. duplicated RoIs (same argmax pixels across
+    RoIs and bins), images with 0 / fewer than 8 / 8k+r RoIs."""
+    from replication_faster_rcnn_amd.ops import _roi_pool_bwd
+    r = np.random.default_rng(7)
+    N, C, H, W = 4, 20, 38, 38
+    x = torch.from_numpy(r.standard_normal((N, C, H, W), dtype=np.float32)).to(DEV)
+    per = [0, 5, 8, 77]
+    rows = []
+    for b, k in enumerate(per):
+        for _ in range(k):
+            x0, y0 = r.uniform(-2, 30, 2)
+            w, h = r.uniform(0, 20, 2)
+            rows.append([b, x0, y0, x0 + w, y0 + h])
+    rows += rows[-10:]  # duplicates in the last image
+    rois = torch.tensor(rows, dtype=torch.float32, device=DEV)
+    out, am = ops.roi_pool_with_argmax(x, rois, 7)
+    g = torch.randn(out.shape, device=DEV)
+    a = _roi_pool_bwd(g, rois, am, x.shape, 1.0)
+    monkeypatch.setenv("FRCNN_BWD_VARIANT", "plain")
+    b = _roi_pool_bwd(g, rois, am, x.shape, 1.0)
+    assert torch.equal(a, b)
+    ref = orc.roi_pool_backward(g.cpu().numpy(), rois.cpu().numpy(), am.cpu().numpy(), x.shape)
+    assert np.array_equal(a.cpu().numpy(), ref)

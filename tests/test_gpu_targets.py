@@ -153,3 +153,46 @@ def test_targets_no_gt(rng_guard):
     ref = orc.proposal_target(roi, np.zeros((0, 4)), np.zeros(0))
     for a, b in zip(out, ref):
         assert np.array_equal(a, b)
+
+
+def test_device_resident_rng_stream(rng_guard):
+    """``rng=`` (device MT19937 state, no host round trip) gives the same
+    samples as the host-RNG path over two chained steps (AT then PT, twice), and
+    the device state ends where numpy's global state does."""
+    N, G, img = 3, 32, 600
+    anchors = orc.generate_anchors(orc.generate_anchor_base(), 16, 38, 38)
+    at = torch.from_numpy(anchors).cuda()
+    bl = [synth.gt_boxes(img, img, G, 4, i, n_valid=[32, 5, 17][i]) for i in range(N)]
+    boxes = torch.from_numpy(np.stack([b for b, _ in bl])).cuda()
+    labels = torch.from_numpy(np.stack([l for _, l in bl])).cuda()
+    rois = []
+    for i in range(N):
+        r, _ = orc.propose_one(anchors, synth.rpn_scores(len(anchors), 4, i),
+                               synth.rpn_deltas(len(anchors), 4, i), img, img, 12000, 600)
+        rois.append(r)
+    rp = np.zeros((N, max(len(r) for r in rois), 4), np.float32)
+    for i, r in enumerate(rois):
+        rp[i, :len(r)] = r
+    rp = torch.from_numpy(rp).cuda()
+    cnt = torch.tensor([len(r) for r in rois], dtype=torch.int32).cuda()
+    np.random.seed(31)
+    host = []
+    for _ in range(2):
+        host.append(targets.anchor_targets(boxes, labels, at))
+        host.append(targets.proposal_targets(rp, cnt, boxes, labels))
+    st_host = np.random.get_state()
+    np.random.seed(31)
+    rng, _ = U.rng_state_to_device(torch.device("cuda"))
+    np.random.seed(999)  # the device stream must not touch numpy's global state
+    dev = []
+    for _ in range(2):
+        dev.append(targets.anchor_targets(boxes, labels, at, rng=rng))
+        dev.append(targets.proposal_targets(rp, cnt, boxes, labels, rng=rng))
+    for h, d in zip(host, dev):
+        for a, b in zip(h, d):
+            assert torch.equal(a, b)
+    buf = rng.cpu().numpy().view(np.uint32)
+    assert np.array_equal(buf[:624], st_host[1]) and int(buf[624]) == st_host[2]
+    st = np.random.get_state()
+    np.random.seed(999)
+    assert np.array_equal(np.random.get_state()[1], st[1])
