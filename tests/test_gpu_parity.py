@@ -473,3 +473,25 @@ def test_roi_pool_bwd_ring_equals_plain(monkeypatch):
     assert torch.equal(a, b)
     ref = orc.roi_pool_backward(g.cpu().numpy(), rois.cpu().numpy(), am.cpu().numpy(), x.shape)
     assert np.array_equal(a.cpu().numpy(), ref)
+
+
+def test_roi_pool_bwd_denormal_and_colliding_grads():
+    """The backward's LDS adds keep IEEE semantics: denormal gradients and sums
+    (no flush to zero), many same-pixel contributions (tiny RoIs whose 49 bins
+    share a few pixels), signed zeros -- bit-identical to the CPU order."""
+    from replication_faster_rcnn_amd.ops import _roi_pool_bwd
+    r = np.random.default_rng(11)
+    N, C, H, W = 2, 6, 10, 10
+    x = torch.from_numpy(r.standard_normal((N, C, H, W), dtype=np.float32)).to(DEV)
+    rows = [[0, 2, 2, 2.4, 2.4], [0, 1, 1, 2, 2], [1, 0, 0, 9, 9], [1, 3, 3, 5, 4]] * 5
+    rows += [[b, *r.uniform(0, 9, 2), *r.uniform(0, 9, 2)] for b in (0, 1) for _ in range(9)]
+    rois = torch.tensor(rows, dtype=torch.float32, device=DEV)
+    out, am = ops.roi_pool_with_argmax(x, rois, 7)
+    g = r.standard_normal(tuple(out.shape)).astype(np.float32)
+    scale = np.where(r.random(g.shape) < 0.5, np.float32(1e-39), np.float32(1.0)).astype(np.float32)
+    g = (g * scale).astype(np.float32)
+    g[r.random(g.shape) < 0.05] = -0.0
+    assert (np.abs(g[g != 0]) < np.finfo(np.float32).tiny).any()
+    gi = _roi_pool_bwd(torch.from_numpy(g).to(DEV), rois, am, x.shape, 1.0)
+    ref = orc.roi_pool_backward(g, rois.cpu().numpy(), am.cpu().numpy(), x.shape)
+    assert np.array_equal(gi.cpu().numpy().view(np.uint32), ref.view(np.uint32))
