@@ -12,11 +12,11 @@
 // with random_interval = "next MT19937 word & mask(i), reject while > i".
 // The caller hands the MT19937 state (624 words + pos) in and gets it back,
 // so the numpy global stream continues exactly as after the reference's calls.
-//  * one wave runs the rejection automaton 64 words at a time: lane l owns
-//    word l; which words are accepted depends on how many earlier lanes
-//    accepted, solved as a fixed point over ballots (<= 64 rounds, ~2-3);
-//  * the twist is done by the same wave, 64 state words per step (the
-//    recurrence reaches back 227 / forward 397 words, both > 64);
+//  * one 1024-thread workgroup runs the rejection automaton a whole 624-word
+//    state block at a time: thread t owns word t; which words are accepted
+//    depends on how many earlier words were, solved as a fixed point over
+//    block prefix counts (a few rounds); the twist is a 3-phase parallel
+//    update of the same block (fy_steps_block / mt_twist_block);
 //  * only the permutation positions the caller needs are reconstructed, by
 //    tracing each position backwards through the recorded swaps (lanes in
 //    parallel): the last m positions for AnchorTarget (which m elements
@@ -253,81 +253,207 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
     return y;
 }
 
-// One wave regenerates the 624-word state in place (numpy mt19937_gen).
-__device__ void mt_twist_wave(uint32_t* key) {
-    const int lane = lane_id();
-    for (int c = 0; c < 10; ++c) {
-        const int i = c * 64 + lane;
-        uint32_t nv = 0;
-        if (i < kMtN - 1) {
-            const uint32_t y = (key[i] & 0x80000000u) | (key[i + 1] & 0x7fffffffu);
-            const uint32_t src = i < kMtN - kMtM ? key[i + kMtM] : key[i - (kMtN - kMtM)];
-            nv = src ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (i < kMtN - 1) key[i] = nv;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    if (lane == 0) {
-        const uint32_t y = (key[kMtN - 1] & 0x80000000u) | (key[0] & 0x7fffffffu);
-        key[kMtN - 1] = key[kMtM - 1] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
+// numpy's rk_interval mask: all ones up to the highest set bit of v (v > 0)
 __device__ __forceinline__ uint32_t mask_for(uint32_t v) {
-    v |= v >> 1;
-    v |= v >> 2;
-    v |= v >> 4;
-    v |= v >> 8;
-    v |= v >> 16;
-    return v;
+    return v ? 0xffffffffu >> __builtin_clz(v) : 0u;
 }
 
-// Run Fisher-Yates steps i = i_hi .. i_lo (descending) on the stream; for
-// steps with i >= rec_lo store J[i - rec_lo] = j.  Wave-uniform; `pos` is the
-// stream position (shared scalar), state in `key`.
-__device__ void fy_steps_wave(uint32_t* key, int& pos, int i_hi, int i_lo, int rec_lo, int* J) {
-    const int lane = lane_id();
+// ---------------------------------------------------- workgroup-wide stream
+// The sampler kernels run as ONE 1024-thread workgroup (the MT19937 stream is
+// a single sequential resource: image n's draws start where image n-1's
+// ended).  Per 624-word state block: a 3-phase parallel twist, then the whole
+// block's rejection automaton solved at once (instead of 64 words per wave
+// step): thread t owns word t; step(t) = i_cur - #accepted(words < t), and
+// accept(t) = (w_t & mask(step)) <= step.  Starting from "all accepted", the
+// Jacobi iteration accept <- f(prefix(accept)) reaches the unique fixed point
+// (word t's decision depends only on words < t) in a few block scans, since a
+// rejection shifts later steps by one and only flips words near a bound.
+constexpr int kSampThreads = 1024;
+// tools-only timeline probe of the sampler (tools/probe_sampler.py): per
+// 624-word block [start, after twist, after fixed point, iterations]
+__device__ int g_samp_probe_on;
+__device__ int g_samp_probe_n;
+__device__ unsigned long long g_samp_probe[4 * 2048];
+constexpr int kSampWaves = kSampThreads / 64;
+
+struct StreamLds {
+    uint32_t key[kMtN];
+    // per-wave accepted counts, triple-buffered by iteration (read as int4s)
+    __attribute__((aligned(16))) int wsum[3][kSampWaves];
+    int last[kSampWaves];     // per-wave highest accepted word index + 1
+    int pos;                  // next unused word of key[]
+};
+
+// numpy mt19937_gen over the whole block: new[i] depends on old[i], old[i+1]
+// and old[i+397] (i < 227) or new[i-227]; three phases of independent words.
+__device__ void mt_twist_block(StreamLds& S) {
+    const int tid = threadIdx.x;
+    auto gen = [&](int i, uint32_t nxt) {
+        const uint32_t y = (S.key[i] & 0x80000000u) | (nxt & 0x7fffffffu);
+        const uint32_t src = i < kMtN - kMtM ? S.key[i + kMtM] : S.key[i - (kMtN - kMtM)];
+        return src ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    };
+    constexpr int kA = kMtN - kMtM;  // 227
+    uint32_t v = 0;
+    if (tid < kA) v = gen(tid, S.key[tid + 1]);
+    __syncthreads();
+    if (tid < kA) S.key[tid] = v;
+    __syncthreads();
+    if (tid < kA) v = gen(kA + tid, S.key[kA + tid + 1]);
+    __syncthreads();
+    if (tid < kA) S.key[kA + tid] = v;
+    __syncthreads();
+    const int i3 = 2 * kA + tid;  // 454 .. 623
+    if (i3 < kMtN) v = gen(i3, i3 + 1 < kMtN ? S.key[i3 + 1] : S.key[0]);
+    __syncthreads();
+    if (i3 < kMtN) S.key[i3] = v;
+    __syncthreads();
+}
+
+// Fisher-Yates steps i = i_hi .. i_lo (descending) of one choice() call, on the
+// stream in S; for steps i >= rec_lo store J[i - rec_lo] = j.  Block-uniform.
+// Two-level fixed point: each wave solves its 64 words exactly for an assumed
+// count of accepted words before it (ballot rounds, no barrier), then one
+// barrier publishes the waves' totals; every thread recomputes all incoming
+// counts from them, and the block stops when no wave's total changed.
+__device__ void fy_steps_block(StreamLds& S, int i_hi, int i_lo, int rec_lo, int* J) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     int i_cur = i_hi;
+    // Iteration `it` writes wsum[it % 3] and reads it plus wsum[(it + 2) % 3]
+    // (the previous totals); a wave one iteration ahead writes the third, so
+    // one barrier per iteration suffices.  "Previous" starts as 64 per wave:
+    // the totals the initial guess (every word accepted) assumes.
+    int it = 0;
+    __syncthreads();
     while (i_cur >= i_lo) {
-        if (pos == kMtN) {
-            mt_twist_wave(key);
-            pos = 0;
+        const bool probe = g_samp_probe_on != 0;
+        unsigned long long pt0 = probe ? __builtin_amdgcn_s_memrealtime() : 0ull, pt1 = pt0;
+        const int it0 = it;
+        if (S.pos == kMtN) {
+            mt_twist_block(S);
+            if (tid == 0) S.pos = 0;
+            __syncthreads();
+            if (probe) pt1 = __builtin_amdgcn_s_memrealtime();
         }
-        const int cnt = min(64, kMtN - pos);
-        const uint32_t w = lane < cnt ? mt_temper(key[pos + lane]) : 0u;
-        uint64_t acc = cnt == 64 ? ~0ull : ((1ull << cnt) - 1ull);
-        int il = 0;
+        const int pos = S.pos;
+        const int cnt = kMtN - pos;
+        const bool word = tid < cnt;
+        const uint32_t w = word ? mt_temper(S.key[pos + tid]) : 0u;
+        // Initial guess of the accepted words before wave q: the expected
+        // acceptance rate at the current step, (i+1) / (mask(i)+1), times 64q.
+        // "Previous" totals are written consistent with it, so a correct guess
+        // converges in one round.
+        const float p_acc = (static_cast<float>(i_cur) + 1.0f) /
+                            (static_cast<float>(mask_for(static_cast<uint32_t>(i_cur))) + 1.0f);
+        auto guess = [&](int q) {  // expected accepted words of wave q
+            const int words = min(max(cnt - 64 * q, 0), 64);
+            return static_cast<int>(static_cast<float>(words) * p_acc);
+        };
+        int base = 0;
+        for (int q = 0; q < wid; ++q) base += guess(q);
+        if (tid < kSampWaves) S.wsum[(it + 2) % 3][tid] = guess(tid);
+        __syncthreads();
+        const bool has_words = wid * 64 < cnt;  // waves past the block's words idle
+        uint64_t bal = __ballot(word);
+        int il = 0, total = 0;
         uint32_t m = 0;
-        bool a = false;
-        for (int it = 0; it < 65; ++it) {
-            il = i_cur - __popcll(acc & lanemask_lt());
-            const bool valid = lane < cnt && il >= i_lo;
-            m = valid ? mask_for(static_cast<uint32_t>(il)) : 0u;
-            a = valid && (w & m) <= static_cast<uint32_t>(il);
-            const uint64_t acc2 = __ballot(a);
-            if (acc2 == acc) break;
-            acc = acc2;
+        bool acc = word;
+        for (;;) {
+            for (; has_words;) {  // this wave's words, exact for the assumed `base`
+                il = i_cur - base - __popcll(bal & lanemask_lt());
+                const bool valid = word && il >= i_lo;
+                m = valid ? mask_for(static_cast<uint32_t>(il)) : 0u;
+                acc = valid && (w & m) <= static_cast<uint32_t>(il);
+                const uint64_t b2 = __ballot(acc);
+                if (b2 == bal) break;
+                bal = b2;
+            }
+            int* ws = S.wsum[it % 3];
+            const int* wp = S.wsum[(it + 2) % 3];
+            if (lane == 0) ws[wid] = __popcll(bal);
+            __syncthreads();
+            // all 2 x 16 totals in 8 independent ds_read_b128 (one LDS round
+            // trip; element-wise reads cost ~1 us per iteration)
+            int4 cur4[kSampWaves / 4], prv4[kSampWaves / 4];
+#pragma unroll
+            for (int q = 0; q < kSampWaves / 4; ++q) {
+                cur4[q] = reinterpret_cast<const int4*>(ws)[q];
+                prv4[q] = reinterpret_cast<const int4*>(wp)[q];
+            }
+            int nb = 0;
+            bool changed = false;
+            total = 0;
+#pragma unroll
+            for (int q = 0; q < kSampWaves / 4; ++q) {
+                const int v[4] = {cur4[q].x, cur4[q].y, cur4[q].z, cur4[q].w};
+                const int u[4] = {prv4[q].x, prv4[q].y, prv4[q].z, prv4[q].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    nb += 4 * q + e < wid ? v[e] : 0;
+                    total += v[e];
+                    changed |= v[e] != u[e];
+                }
+            }
+            base = nb;
+            ++it;
+            if (!changed) break;  // block-uniform: every thread read the same totals
         }
-        if (a && il >= rec_lo) J[il - rec_lo] = static_cast<int>(w & m);
-        const int na = __popcll(acc);
+        if (probe && tid == 0) {
+            const int slot = g_samp_probe_n;
+            if (slot < 2048) {
+                g_samp_probe[4 * slot + 0] = pt0;
+                g_samp_probe[4 * slot + 1] = pt1;
+                g_samp_probe[4 * slot + 2] = __builtin_amdgcn_s_memrealtime();
+                g_samp_probe[4 * slot + 3] = static_cast<unsigned long long>(it - it0);
+                g_samp_probe_n = slot + 1;
+            }
+        }
+        // acc / il / m are the fixed point's (computed from the final base)
+        if (acc && il >= rec_lo) J[il - rec_lo] = static_cast<int>(w & m);
         int consumed = cnt;
-        if (i_cur - na < i_lo) consumed = 64 - __clzll(acc);  // last accepted lane + 1
-        i_cur -= na;
-        pos += consumed;
+        if (i_cur - total < i_lo) {  // the call ends inside this block
+            if (lane == 0) S.last[wid] = bal ? wid * 64 + 64 - __clzll(bal) : 0;
+            __syncthreads();
+            consumed = 0;
+            for (int q = 0; q < kSampWaves; ++q) consumed = max(consumed, S.last[q]);
+        }
+        i_cur -= total;
+        __syncthreads();  // everyone has read S.pos / S.last / the totals
+        if (tid == 0) S.pos = pos + consumed;
+        __syncthreads();
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 // Final value at permutation position p (identity start), given J[i - rec_lo]
 // for every step i >= rec_lo of the n-element shuffle.  Requires p >= rec_lo.
+// J must be 16-byte aligned: the swaps are read four at a time (ds_read_b128),
+// so a thread has 4 independent LDS reads in flight per 4 steps instead of one
+// dependent read per step (the ProposalTarget trace runs ~600 steps per
+// position).
 __device__ __forceinline__ int fy_trace(int p, int n, int rec_lo, const int* J) {
     int cur = p;
-    for (int i = (p > 1 ? p : 1); i < n; ++i) {
+    int i = p > 1 ? p : 1;
+    for (; i < n && ((i - rec_lo) & 3); ++i) {
         const int j = J[i - rec_lo];
-        if (cur == i) cur = j;
-        else if (cur == j) cur = i;
+        cur = cur == i ? j : (cur == j ? i : cur);
+    }
+    const int4* J4 = reinterpret_cast<const int4*>(J + (i - rec_lo));
+    for (; i + 16 <= n; i += 16, J4 += 4) {
+        int4 q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) q[u] = J4[u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int b = i + 4 * u;
+            cur = cur == b ? q[u].x : (cur == q[u].x ? b : cur);
+            cur = cur == b + 1 ? q[u].y : (cur == q[u].y ? b + 1 : cur);
+            cur = cur == b + 2 ? q[u].z : (cur == q[u].z ? b + 2 : cur);
+            cur = cur == b + 3 ? q[u].w : (cur == q[u].w ? b + 3 : cur);
+        }
+    }
+    for (; i < n; ++i) {
+        const int j = J[i - rec_lo];
+        cur = cur == i ? j : (cur == j ? i : cur);
     }
     return cur;
 }
@@ -338,16 +464,15 @@ __device__ __forceinline__ int fy_trace(int p, int n, int rec_lo, const int* J) 
 // the caller); pos_sampled / neg_sampled record whether a call happened.
 constexpr int kMaxKeep = 4096;
 
-__global__ __launch_bounds__(256) void at_sample_kernel(
+__global__ __launch_bounds__(kSampThreads) void at_sample_kernel(
     int N, int A, int n_sample, int n_pos_max, const int* __restrict__ pos_list,
     const int* __restrict__ neg_list, const int* __restrict__ npos, const int* __restrict__ nneg,
     uint32_t* __restrict__ rng, uint8_t* __restrict__ keep, int* __restrict__ sampled) {
-    __shared__ uint32_t key[kMtN];
-    __shared__ int J[kMaxKeep];
-    __shared__ int s_pos;
-    const int tid = threadIdx.x, wid = tid >> 6;
-    for (int i = tid; i < kMtN; i += 256) key[i] = rng[i];
-    if (tid == 0) s_pos = static_cast<int>(rng[kMtN]);
+    __shared__ StreamLds S;
+    __shared__ __attribute__((aligned(16))) int J[kMaxKeep];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kMtN; i += kSampThreads) S.key[i] = rng[i];
+    if (tid == 0) S.pos = static_cast<int>(rng[kMtN]);
     __syncthreads();
     for (int n = 0; n < N; ++n) {
         const int P = npos[n];
@@ -361,22 +486,18 @@ __global__ __launch_bounds__(256) void at_sample_kernel(
             if (tid == 0) sampled[2 * n + call] = do_call ? 1 : 0;
             if (!do_call) continue;
             const int k = cnt - m;  // disabled = perm[:k]; survivors = perm[k:]
-            if (wid == 0) {
-                int pos = s_pos;
-                fy_steps_wave(key, pos, cnt - 1, 1, k, J);
-                if (lane_id() == 0) s_pos = pos;
-            }
+            fy_steps_block(S, cnt - 1, 1, k, J);
             __syncthreads();
             const int* lst = (call == 0 ? pos_list : neg_list) + static_cast<size_t>(n) * A;
-            for (int p = k + tid; p < cnt; p += 256) {  // survivors, any order
+            for (int p = k + tid; p < cnt; p += kSampThreads) {  // survivors, any order
                 const int v = fy_trace(p, cnt, k, J);  // p >= k >= 1
                 keep[static_cast<size_t>(n) * A + lst[v]] = 1;
             }
             __syncthreads();
         }
     }
-    for (int i = tid; i < kMtN; i += 256) rng[i] = key[i];
-    if (tid == 0) rng[kMtN] = static_cast<uint32_t>(s_pos);
+    for (int i = tid; i < kMtN; i += kSampThreads) rng[i] = S.key[i];
+    if (tid == 0) rng[kMtN] = static_cast<uint32_t>(S.pos);
 }
 
 // grid (ceil(A/256), N): final label (after disabling) and regression target
@@ -499,17 +620,16 @@ __global__ __launch_bounds__(1024) void pt_iou_kernel(
 
 // One workgroup: the two choice() calls of utils/utils.py:248-258 per image,
 // in image order; sample order = pos perm prefix, then neg perm prefix.
-__global__ __launch_bounds__(256) void pt_sample_kernel(
+__global__ __launch_bounds__(kSampThreads) void pt_sample_kernel(
     int N, int stride, int n_sample, int pos_per_image, const int* __restrict__ pos_list,
     const int* __restrict__ neg_list, const int* __restrict__ npos, const int* __restrict__ nneg,
     uint32_t* __restrict__ rng, int* __restrict__ sample, int* __restrict__ scount,
     int* __restrict__ spos) {
-    __shared__ uint32_t key[kMtN];
-    __shared__ int J[kMaxKeep];
-    __shared__ int s_pos;
-    const int tid = threadIdx.x, wid = tid >> 6;
-    for (int i = tid; i < kMtN; i += 256) key[i] = rng[i];
-    if (tid == 0) s_pos = static_cast<int>(rng[kMtN]);
+    __shared__ StreamLds S;
+    __shared__ __attribute__((aligned(16))) int J[kMaxKeep];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kMtN; i += kSampThreads) S.key[i] = rng[i];
+    if (tid == 0) S.pos = static_cast<int>(rng[kMtN]);
     __syncthreads();
     for (int n = 0; n < N; ++n) {
         const int P = npos[n], Q = nneg[n];
@@ -522,22 +642,10 @@ __global__ __launch_bounds__(256) void pt_sample_kernel(
             const int k = call == 0 ? kp : kn;
             const int off = call == 0 ? 0 : kp;
             if (cnt == 0) continue;
-            if (wid == 0) {
-                int pos = s_pos;
-                fy_steps_wave(key, pos, cnt - 1, 1, 1, J);  // every step: J[i-1]
-                if (lane_id() == 0) s_pos = pos;
-            }
+            fy_steps_block(S, cnt - 1, 1, 1, J);  // every step: J[i-1]
             __syncthreads();
             const int* lst = (call == 0 ? pos_list : neg_list) + static_cast<size_t>(n) * stride;
-            for (int p = tid; p < k; p += 256) {
-                int cur = p;
-                for (int i = (p > 1 ? p : 1); i < cnt; ++i) {
-                    const int j = J[i - 1];
-                    if (cur == i) cur = j;
-                    else if (cur == j) cur = i;
-                }
-                out[off + p] = lst[cur];
-            }
+            for (int p = tid; p < k; p += kSampThreads) out[off + p] = lst[fy_trace(p, cnt, 1, J)];
             __syncthreads();
         }
         if (tid == 0) {
@@ -545,8 +653,8 @@ __global__ __launch_bounds__(256) void pt_sample_kernel(
             spos[n] = kp;
         }
     }
-    for (int i = tid; i < kMtN; i += 256) rng[i] = key[i];
-    if (tid == 0) rng[kMtN] = static_cast<uint32_t>(s_pos);
+    for (int i = tid; i < kMtN; i += kSampThreads) rng[i] = S.key[i];
+    if (tid == 0) rng[kMtN] = static_cast<uint32_t>(S.pos);
 }
 
 // grid N x n_sample: sample_roi, normalised gt_roi_reg and gt_roi_label
@@ -737,7 +845,7 @@ extern "C" int frcnn_anchor_target(int N, int A, int G, const float* anchors, co
     if (hipMemsetAsync(w.keep, 0, static_cast<size_t>(N) * A, st) != hipSuccess)
         return check_launch("frcnn_anchor_target memset");
     if (rng_state) {
-        hipLaunchKernelGGL(at_sample_kernel, dim3(1), dim3(256), 0, st, N, A, n_sample, n_pos_max,
+        hipLaunchKernelGGL(at_sample_kernel, dim3(1), dim3(kSampThreads), 0, st, N, A, n_sample, n_pos_max,
                            w.pos_list, w.neg_list, w.npos, w.nneg, rng_state, w.keep, w.sampled);
         FRCNN_LAUNCH_CHECK("at_sample_kernel");
     } else if (hipMemsetAsync(w.sampled, 0, sizeof(int) * 2 * N, st) != hipSuccess) {
@@ -829,7 +937,7 @@ extern "C" int frcnn_proposal_target(int N, int Rp, const float* rois, const int
                        w.roi_all, w.assign, w.pos_list, w.neg_list, w.npos, w.nneg);
     FRCNN_LAUNCH_CHECK("pt_iou_kernel");
     const int pos_per_image = static_cast<int>(std::nearbyint(n_sample * pos_ratio));  // np.round
-    hipLaunchKernelGGL(pt_sample_kernel, dim3(1), dim3(256), 0, st, N, stride, n_sample,
+    hipLaunchKernelGGL(pt_sample_kernel, dim3(1), dim3(kSampThreads), 0, st, N, stride, n_sample,
                        pos_per_image, w.pos_list, w.neg_list, w.npos, w.nneg, rng_state, w.sample,
                        sample_count, w.spos);
     FRCNN_LAUNCH_CHECK("pt_sample_kernel");
@@ -894,4 +1002,20 @@ extern "C" int frcnn_bbox2reg(const void* anchors, int a_is_f64, const void* bbo
                            static_cast<const double*>(anchors), static_cast<const double*>(bbox), n, out);
     FRCNN_LAUNCH_CHECK("bbox2reg_kernel");
     return FRCNN_OK;
+}
+
+// tools-only (not part of the C-ABI): sampler timeline probe
+extern "C" int frcnn_dbg_samp_probe(int on, unsigned long long* host, int n) {
+    if (host) {
+        if (n > 4 * 2048) n = 4 * 2048;
+        if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_samp_probe), sizeof(unsigned long long) * n) != hipSuccess)
+            return -2;
+        int cnt = 0;
+        if (hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(g_samp_probe_n), sizeof(int)) != hipSuccess) return -2;
+        return cnt;
+    }
+    const int zero = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_samp_probe_n), &zero, sizeof(int)) != hipSuccess) return -2;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_samp_probe_on), &on, sizeof(int)) != hipSuccess) return -2;
+    return 0;
 }
