@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--streams", type=int, default=2, choices=(1, 2),
                     help="2: the proposal layer of step k+1 runs on its own HIP stream beside "
                          "step k's RoIPool (each step still does all of its work)")
+    ap.add_argument("--prop-cus", type=int, default=0,
+                    help="with --streams 2: run the proposal stream on this many CUs and the "
+                         "RoIPool stream on the rest (hipExtStreamCreateWithCUMask); 0 = shared")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-baseline sample (rank 0, N=1 only); 0 disables")
     return ap.parse_args()
@@ -152,6 +155,24 @@ def cpu_baseline_train(cfg, seconds):
                       f"{el:.1f} s on {os.cpu_count()}-cpu host"}
 
 
+def make_streams(args, device):
+    """(proposal stream, RoIPool stream).  --streams 1: both the current
+    stream.  --prop-cus K: a CU partition -- K CUs for the latency-bound
+    proposal layer (spread so that every XCD and every 8-CU block gets its
+    share whichever way the mask bits map to XCDs), the rest for the pool."""
+    if args.streams == 1:
+        s = torch.cuda.current_stream()
+        return s, s
+    if args.prop_cus <= 0:
+        return torch.cuda.Stream(), torch.cuda.Stream()
+    from replication_faster_rcnn_amd import _lib
+    n = _lib.cu_count()
+    k = min(args.prop_cus, n // 2)
+    prop = sorted({(j * 8 + (j % 8)) % n for j in range(k)})
+    pool = [i for i in range(n) if i not in set(prop)]
+    return _lib.cu_masked_stream(prop, device), _lib.cu_masked_stream(pool, device)
+
+
 def inference_step_fn(args, c, sc, de, x, base, world, ev):
     """cfg1-4: propose -> (RCCL all-gather of detections) -> RoI transform +
     pack + RoIPool forward (nets/rpn.py:102-138, nets/heads.py:42-48)."""
@@ -164,8 +185,7 @@ def inference_step_fn(args, c, sc, de, x, base, world, ev):
     # (measured: stream priorities change nothing; holding step k+1's proposals
     # until step k's pool is issued gives the pool the whole chip, 68 vs 75 us,
     # but costs 17 % of the throughput)
-    s_prop = torch.cuda.current_stream() if args.streams == 1 else torch.cuda.Stream()
-    s_pool = torch.cuda.current_stream() if args.streams == 1 else torch.cuda.Stream()
+    s_prop, s_pool = make_streams(args, dev)
 
     def step(timed):
         with torch.cuda.stream(s_prop):
@@ -213,8 +233,7 @@ def train_step_fn(args, c, sc, de, x, base, world, ev, first_image):
     gen = torch.Generator(device=dev)
     gen.manual_seed(1)
     grad = torch.randn((N * S, x.size(1), 7, 7), device=dev, generator=gen)
-    s_prop = torch.cuda.current_stream() if args.streams == 1 else torch.cuda.Stream()
-    s_pool = torch.cuda.current_stream() if args.streams == 1 else torch.cuda.Stream()
+    s_prop, s_pool = make_streams(args, dev)
     state = {}
 
     def step(timed):
@@ -315,7 +334,8 @@ def main():
         "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
         "config": {"workload": workload, "global_batch": world * N,
-                   "parallelism": f"dp{world} (per-image sharding)", "streams": args.streams},
+                   "parallelism": f"dp{world} (per-image sharding)", "streams": args.streams,
+                   "prop_cus": args.prop_cus if args.streams == 2 else 0},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "roi_pool_bwd_kernel" if train else "roi_pool_fwd_px8q_kernel<head>",

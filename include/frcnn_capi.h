@@ -34,6 +34,15 @@ extern "C" {
 const char* frcnn_version(void);
 const char* frcnn_last_error(void);
 
+/* Runtime helpers (no reference counterpart: the reference runs one image at
+ * a time on the host).  CU count of the current device, and HIP streams
+ * restricted to a CU subset (bit i of cu_mask = CU i, n_words 32-bit words) so
+ * that the proposal layer and the RoIPool of consecutive steps can share the
+ * chip by partition.  Destroy with frcnn_stream_destroy. */
+int frcnn_device_cu_count(int* out);
+int frcnn_stream_create_cu_masked(const uint32_t* cu_mask, int n_words, void** stream);
+int frcnn_stream_destroy(void* stream);
+
 /* ---------------------------------------------------------------- anchors */
 
 /* utils/anchors.py:5 generate_anchor_base(base_size, ratios, anchor_scales).

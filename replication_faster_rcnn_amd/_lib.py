@@ -39,6 +39,9 @@ class ProposeParams(ctypes.Structure):
 SIGNATURES = {
     "frcnn_version": (ctypes.c_char_p, []),
     "frcnn_last_error": (ctypes.c_char_p, []),
+    "frcnn_device_cu_count": (I32, [P]),
+    "frcnn_stream_create_cu_masked": (I32, [P, I32, P]),
+    "frcnn_stream_destroy": (I32, [P]),
     "frcnn_anchor_base": (I32, [P, I32, P, I32, F64, P, P]),
     "frcnn_generate_anchors": (I32, [P, I32, I32, I32, I32, P, P]),
     "frcnn_reg2bbox": (I32, [P, P, I64, P, P]),
@@ -111,3 +114,24 @@ def device():
 
 def workspace(nbytes: int, dev) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
+
+
+def cu_count() -> int:
+    lib = load()
+    n = ctypes.c_int(0)
+    check(lib.frcnn_device_cu_count(ctypes.byref(n)), "device_cu_count")
+    return int(n.value)
+
+
+def cu_masked_stream(cus, device=None):
+    """A torch stream (ExternalStream) whose kernels run only on the given CU
+    indices (hipExtStreamCreateWithCUMask).  The HIP stream lives as long as
+    the process (streams are few and long-lived)."""
+    lib = load()
+    n_words = (max(cus) // 32 + 1) if cus else 1
+    mask = (ctypes.c_uint32 * n_words)()
+    for c in cus:
+        mask[c // 32] |= 1 << (c % 32)
+    h = ctypes.c_void_p(0)
+    check(lib.frcnn_stream_create_cu_masked(mask, n_words, ctypes.byref(h)), "stream_create_cu_masked")
+    return torch.cuda.ExternalStream(h.value, device=device)
