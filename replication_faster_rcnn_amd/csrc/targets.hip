@@ -258,30 +258,33 @@ __device__ __forceinline__ uint32_t mask_for(uint32_t v) {
     return v ? 0xffffffffu >> __builtin_clz(v) : 0u;
 }
 
-// ---------------------------------------------------- workgroup-wide stream
-// The sampler kernels run as ONE 1024-thread workgroup (the MT19937 stream is
-// a single sequential resource: image n's draws start where image n-1's
-// ended).  Per 624-word state block: a 3-phase parallel twist, then the whole
-// block's rejection automaton solved at once (instead of 64 words per wave
-// step): thread t owns word t; step(t) = i_cur - #accepted(words < t), and
-// accept(t) = (w_t & mask(step)) <= step.  Starting from "all accepted", the
-// Jacobi iteration accept <- f(prefix(accept)) reaches the unique fixed point
-// (word t's decision depends only on words < t) in a few block scans, since a
-// rejection shifts later steps by one and only flips words near a bound.
-constexpr int kSampThreads = 1024;
+// ------------------------------------------------------------ stream walker
+// The sampler kernels run as ONE 256-thread workgroup (the MT19937 stream is a
+// single sequential resource: image n's draws start where image n-1's
+// ended).  Per 624-word state block: a 3-phase parallel twist by the whole
+// workgroup, then ONE wave runs the rejection automaton over the block, 256
+// words per round (4 per lane, 4 independent ballot chains for ILP): word t's
+// step is i_cur - #accepted(words < t), accept(t) = (w_t & mask(step)) <=
+// step; starting from "all accepted", the iteration accept <- f(prefix(accept))
+// reaches the unique fixed point (word t depends only on words < t) in a few
+// rounds, since a rejection shifts later steps by one and only flips words
+// near a bound.  Measured per block (tools/probe_sampler.py): 16 waves with a
+// barrier per round ~4 us, one wave alone ~2.6-3.3 us (issue bound), 4 waves.
+constexpr int kSampThreads = 256;
+constexpr int kSampWaves = kSampThreads / 64;  // 4: one per SIMD
+constexpr int kWpl = 3;                        // words per lane
+constexpr int kSeg = kWpl * 64;                // words per wave segment (4 x 192 >= 624)
 // tools-only timeline probe of the sampler (tools/probe_sampler.py): per
-// 624-word block [start, after twist, after fixed point, iterations]
+// 624-word block [start, after twist, after automaton, rounds]
 __device__ int g_samp_probe_on;
 __device__ int g_samp_probe_n;
 __device__ unsigned long long g_samp_probe[4 * 2048];
-constexpr int kSampWaves = kSampThreads / 64;
 
 struct StreamLds {
     uint32_t key[kMtN];
-    // per-wave accepted counts, triple-buffered by iteration (read as int4s)
-    __attribute__((aligned(16))) int wsum[3][kSampWaves];
-    int last[kSampWaves];     // per-wave highest accepted word index + 1
-    int pos;                  // next unused word of key[]
+    __attribute__((aligned(16))) int tot[3][kSampWaves];  // segment totals, by round
+    __attribute__((aligned(16))) int last[kSampWaves];    // highest accepted word + 1
+    int pos;                                             // next unused word of key[]
 };
 
 // numpy mt19937_gen over the whole block: new[i] depends on old[i], old[i+1]
@@ -293,7 +296,7 @@ __device__ void mt_twist_block(StreamLds& S) {
         const uint32_t src = i < kMtN - kMtM ? S.key[i + kMtM] : S.key[i - (kMtN - kMtM)];
         return src ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
     };
-    constexpr int kA = kMtN - kMtM;  // 227
+    constexpr int kA = kMtN - kMtM;  // 227 <= kSampThreads
     uint32_t v = 0;
     if (tid < kA) v = gen(tid, S.key[tid + 1]);
     __syncthreads();
@@ -311,24 +314,20 @@ __device__ void mt_twist_block(StreamLds& S) {
 }
 
 // Fisher-Yates steps i = i_hi .. i_lo (descending) of one choice() call, on the
-// stream in S; for steps i >= rec_lo store J[i - rec_lo] = j.  Block-uniform.
-// Two-level fixed point: each wave solves its 64 words exactly for an assumed
-// count of accepted words before it (ballot rounds, no barrier), then one
-// barrier publishes the waves' totals; every thread recomputes all incoming
-// counts from them, and the block stops when no wave's total changed.
+// stream in S; for steps i >= rec_lo store J[i - rec_lo] = j.  Called by the
+// whole workgroup (block-uniform).  Per 624-word block the 4 waves (one per
+// SIMD) own 192-word segments; a round solves every segment exactly for an
+// assumed count of accepted words before it (ballot fixed point inside the
+// wave), then one barrier publishes the segment totals; the block is done when
+// no total changed.  The starting point is the expected acceptance rate, so
+// most blocks take one round.
 __device__ void fy_steps_block(StreamLds& S, int i_hi, int i_lo, int rec_lo, int* J) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     int i_cur = i_hi;
-    // Iteration `it` writes wsum[it % 3] and reads it plus wsum[(it + 2) % 3]
-    // (the previous totals); a wave one iteration ahead writes the third, so
-    // one barrier per iteration suffices.  "Previous" starts as 64 per wave:
-    // the totals the initial guess (every word accepted) assumes.
-    int it = 0;
-    __syncthreads();
-    while (i_cur >= i_lo) {
+    int it = 0;  // round counter: round r writes tot[r % 3], reads tot[(r + 2) % 3]
+    while (i_cur >= i_lo) {  // block-uniform: every thread tracks the same i_cur
         const bool probe = g_samp_probe_on != 0;
         unsigned long long pt0 = probe ? __builtin_amdgcn_s_memrealtime() : 0ull, pt1 = pt0;
-        const int it0 = it;
         if (S.pos == kMtN) {
             mt_twist_block(S);
             if (tid == 0) S.pos = 0;
@@ -337,87 +336,94 @@ __device__ void fy_steps_block(StreamLds& S, int i_hi, int i_lo, int rec_lo, int
         }
         const int pos = S.pos;
         const int cnt = kMtN - pos;
-        const bool word = tid < cnt;
-        const uint32_t w = word ? mt_temper(S.key[pos + tid]) : 0u;
-        // Initial guess of the accepted words before wave q: the expected
-        // acceptance rate at the current step, (i+1) / (mask(i)+1), times 64q.
-        // "Previous" totals are written consistent with it, so a correct guess
-        // converges in one round.
         const float p_acc = (static_cast<float>(i_cur) + 1.0f) /
                             (static_cast<float>(mask_for(static_cast<uint32_t>(i_cur))) + 1.0f);
-        auto guess = [&](int q) {  // expected accepted words of wave q
-            const int words = min(max(cnt - 64 * q, 0), 64);
-            return static_cast<int>(static_cast<float>(words) * p_acc);
-        };
-        int base = 0;
-        for (int q = 0; q < wid; ++q) base += guess(q);
-        if (tid < kSampWaves) S.wsum[(it + 2) % 3][tid] = guess(tid);
-        __syncthreads();
-        const bool has_words = wid * 64 < cnt;  // waves past the block's words idle
-        uint64_t bal = __ballot(word);
-        int il = 0, total = 0;
-        uint32_t m = 0;
-        bool acc = word;
-        for (;;) {
-            for (; has_words;) {  // this wave's words, exact for the assumed `base`
-                il = i_cur - base - __popcll(bal & lanemask_lt());
-                const bool valid = word && il >= i_lo;
-                m = valid ? mask_for(static_cast<uint32_t>(il)) : 0u;
-                acc = valid && (w & m) <= static_cast<uint32_t>(il);
-                const uint64_t b2 = __ballot(acc);
-                if (b2 == bal) break;
-                bal = b2;
-            }
-            int* ws = S.wsum[it % 3];
-            const int* wp = S.wsum[(it + 2) % 3];
-            if (lane == 0) ws[wid] = __popcll(bal);
-            __syncthreads();
-            // all 2 x 16 totals in 8 independent ds_read_b128 (one LDS round
-            // trip; element-wise reads cost ~1 us per iteration)
-            int4 cur4[kSampWaves / 4], prv4[kSampWaves / 4];
+        auto guess_before = [&](int v) { return static_cast<int>(static_cast<float>(v * kSeg) * p_acc); };
+        uint32_t w[kWpl];
+        uint64_t bal[kWpl];
+        int base = guess_before(wid);
 #pragma unroll
-            for (int q = 0; q < kSampWaves / 4; ++q) {
-                cur4[q] = reinterpret_cast<const int4*>(ws)[q];
-                prv4[q] = reinterpret_cast<const int4*>(wp)[q];
+        for (int q = 0; q < kWpl; ++q) {
+            const int t = wid * kSeg + q * 64 + lane;
+            w[q] = t < cnt ? mt_temper(S.key[pos + t]) : 0u;
+            const int ig = i_cur - static_cast<int>(static_cast<float>(t) * p_acc);
+            const bool v0 = t < cnt && ig >= i_lo;
+            bal[q] = __ballot(v0 && (w[q] & mask_for(static_cast<uint32_t>(ig))) <=
+                                         static_cast<uint32_t>(ig));
+        }
+        if (tid < kSampWaves)  // "previous" totals consistent with the guessed bases
+            S.tot[(it + 2) % 3][tid] = guess_before(tid + 1) - guess_before(tid);
+        __syncthreads();
+        int il[kWpl];
+        uint32_t m[kWpl];
+        bool a[kWpl];
+        int total = 0, rounds = 0;
+        for (;;) {
+            ++rounds;
+            for (;;) {  // this segment, exact for the assumed `base`
+                int b = base;
+#pragma unroll
+                for (int q = 0; q < kWpl; ++q) {
+                    const int t = wid * kSeg + q * 64 + lane;
+                    il[q] = i_cur - b - __popcll(bal[q] & lanemask_lt());
+                    const bool valid = t < cnt && il[q] >= i_lo;
+                    m[q] = valid ? mask_for(static_cast<uint32_t>(il[q])) : 0u;
+                    a[q] = valid && (w[q] & m[q]) <= static_cast<uint32_t>(il[q]);
+                    b += __popcll(bal[q]);
+                }
+                bool same = true;
+#pragma unroll
+                for (int q = 0; q < kWpl; ++q) {
+                    const uint64_t nb = __ballot(a[q]);
+                    same = same && nb == bal[q];
+                    bal[q] = nb;
+                }
+                if (same) break;
             }
-            int nb = 0;
-            bool changed = false;
+            int mine = 0;
+#pragma unroll
+            for (int q = 0; q < kWpl; ++q) mine += __popcll(bal[q]);
+            if (lane == 0) S.tot[it % 3][wid] = mine;
+            __syncthreads();
+            const int4 cur = *reinterpret_cast<const int4*>(S.tot[it % 3]);
+            const int4 prv = *reinterpret_cast<const int4*>(S.tot[(it + 2) % 3]);
+            ++it;
+            const int c4[4] = {cur.x, cur.y, cur.z, cur.w};
+            base = 0;
             total = 0;
 #pragma unroll
-            for (int q = 0; q < kSampWaves / 4; ++q) {
-                const int v[4] = {cur4[q].x, cur4[q].y, cur4[q].z, cur4[q].w};
-                const int u[4] = {prv4[q].x, prv4[q].y, prv4[q].z, prv4[q].w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    nb += 4 * q + e < wid ? v[e] : 0;
-                    total += v[e];
-                    changed |= v[e] != u[e];
-                }
+            for (int v = 0; v < kSampWaves; ++v) {
+                base += v < wid ? c4[v] : 0;
+                total += c4[v];
             }
-            base = nb;
-            ++it;
-            if (!changed) break;  // block-uniform: every thread read the same totals
+            if (cur.x == prv.x && cur.y == prv.y && cur.z == prv.z && cur.w == prv.w) break;
         }
+        // the fixed point: il / m / a are consistent with the final bases
+#pragma unroll
+        for (int q = 0; q < kWpl; ++q)
+            if (a[q] && il[q] >= rec_lo) J[il[q] - rec_lo] = static_cast<int>(w[q] & m[q]);
+        int consumed = cnt;
+        if (i_cur - total < i_lo) {  // the call ends inside this block
+            int last = 0;
+#pragma unroll
+            for (int q = 0; q < kWpl; ++q)
+                if (bal[q]) last = wid * kSeg + q * 64 + 64 - __clzll(bal[q]);
+            if (lane == 0) S.last[wid] = last;
+            __syncthreads();
+            const int4 l4 = *reinterpret_cast<const int4*>(S.last);
+            consumed = max(max(l4.x, l4.y), max(l4.z, l4.w));
+        }
+        i_cur -= total;
         if (probe && tid == 0) {
             const int slot = g_samp_probe_n;
             if (slot < 2048) {
                 g_samp_probe[4 * slot + 0] = pt0;
                 g_samp_probe[4 * slot + 1] = pt1;
                 g_samp_probe[4 * slot + 2] = __builtin_amdgcn_s_memrealtime();
-                g_samp_probe[4 * slot + 3] = static_cast<unsigned long long>(it - it0);
+                g_samp_probe[4 * slot + 3] = static_cast<unsigned long long>(rounds);
                 g_samp_probe_n = slot + 1;
             }
         }
-        // acc / il / m are the fixed point's (computed from the final base)
-        if (acc && il >= rec_lo) J[il - rec_lo] = static_cast<int>(w & m);
-        int consumed = cnt;
-        if (i_cur - total < i_lo) {  // the call ends inside this block
-            if (lane == 0) S.last[wid] = bal ? wid * 64 + 64 - __clzll(bal) : 0;
-            __syncthreads();
-            consumed = 0;
-            for (int q = 0; q < kSampWaves; ++q) consumed = max(consumed, S.last[q]);
-        }
-        i_cur -= total;
         __syncthreads();  // everyone has read S.pos / S.last / the totals
         if (tid == 0) S.pos = pos + consumed;
         __syncthreads();
