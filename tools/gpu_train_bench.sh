@@ -23,6 +23,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 rc=$?; echo "rocprof rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 bash tools/pmc_roi_pool.sh "$OUT/pmc" bench cfg5 && \
-    python3 tools/summarize_pmc.py "$OUT/pmc" roi_pool_bwd_kernel --config cfg5 --json "$OUT/roi_pool_bwd_traffic.json" > "$OUT/pmc_bwd.txt" && \
+    python3 tools/summarize_pmc.py "$OUT/pmc" roi_pool_bwd_pf --config cfg5 --json "$OUT/roi_pool_bwd_traffic.json" > "$OUT/pmc_bwd.txt" && \
     python3 tools/summarize_pmc.py "$OUT/pmc" px8q_kernel --config cfg5 --json "$OUT/roi_pool_fwd_traffic.json" > "$OUT/pmc_fwd.txt" && \
     cat "$OUT/pmc_bwd.txt" "$OUT/pmc_fwd.txt"
