@@ -5,6 +5,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -55,8 +56,9 @@ def test_shard_covers_batch():
         assert got == list(range(n))
 
 
-def test_two_rank_gather_is_p_invariant():
-    world, n_total, post = 2, 4, 50
+@pytest.mark.parametrize("world,n_total", [(2, 4), (4, 8)])
+def test_rank_gather_is_p_invariant(world, n_total):
+    post = 50
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
