@@ -59,6 +59,17 @@ int frcnn_generate_anchors(const float* anchor_base, int K, int feat_stride, int
 /* utils/utils.py:47 reg2bbox(anchors, reg): fp32 [n,4] x [n,4] -> [n,4]. */
 int frcnn_reg2bbox(const float* anchors, const float* reg, int64_t n, float* out, void* stream);
 
+/* nets/rpn.py:117-124 RPN head epilogue, one launch instead of the reference's
+ * permute/contiguous/softmax/slice chain:
+ *   cls fp32 [N, 2K, H, W] (self.cls conv output), reg fp32 [N, 4K, H, W]
+ *   -> cls_nhwc fp32 [N, A, 2]  = cls.permute(0,2,3,1).contiguous().view(N,-1,2)  (:117-118)
+ *      fg       fp32 [N, A]     = F.softmax(cls_nhwc, -1)[:, :, 1]              (:119)
+ *      reg_nhwc fp32 [N, A, 4]  = reg.permute(0,2,3,1).contiguous().view(N,-1,4)  (:123-124)
+ * A = H*W*K, 1 <= K <= 32.  fg feeds frcnn_propose's scores, reg_nhwc its deltas. */
+int frcnn_rpn_head_epilogue(const float* cls, const float* reg, int N, int K, int feat_h,
+                            int feat_w, float* cls_nhwc, float* fg, float* reg_nhwc,
+                            void* stream);
+
 /* ------------------------------------------------------------- proposals */
 
 /* Parameters of the batched proposal layer (nets/rpn.py:22-45 kwargs). */

@@ -111,6 +111,24 @@ def reg2bbox(anchors, reg):
     return np.stack([x - hh, y - hw, x + hh, y + hw], axis=1).astype(np.float32)
 
 
+def rpn_head_epilogue(cls, reg):
+    """nets/rpn.py:117-124: cls fp32 [N,2K,H,W], reg fp32 [N,4K,H,W] ->
+    (cls_nhwc [N,A,2], fg [N,A], reg_nhwc [N,A,4]).  The softmax follows torch's
+    CPU last-dim kernel (ATen _vec_softmax_lastdim): m = max, e = exp(x - m),
+    out = e * (1 / (e0 + e1)), each op fp32; exp correctly rounded (see module
+    docstring -- torch's vectorised exp is host-dependent in its last bits)."""
+    cls = np.asarray(cls, dtype=np.float32)
+    reg = np.asarray(reg, dtype=np.float32)
+    n = cls.shape[0]
+    c = np.ascontiguousarray(cls.transpose(0, 2, 3, 1)).reshape(n, -1, 2)   # :118
+    r = np.ascontiguousarray(reg.transpose(0, 2, 3, 1)).reshape(n, -1, 4)   # :124
+    m = np.maximum(c[:, :, 0], c[:, :, 1])
+    e0 = exp_cr(c[:, :, 0] - m)
+    e1 = exp_cr(c[:, :, 1] - m)
+    inv = np.float32(1) / (e0 + e1)
+    return c, (e1 * inv).astype(np.float32), r                                # :119-120
+
+
 def bbox2reg(anchors, bbox):
     """utils/utils.py:75-100.  Anchor statistics in the anchors' dtype, box
     statistics in the boxes' dtype, output fp64."""

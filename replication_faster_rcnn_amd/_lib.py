@@ -45,7 +45,8 @@ SIGNATURES = {
     "frcnn_anchor_base": (I32, [P, I32, P, I32, F64, P, P]),
     "frcnn_generate_anchors": (I32, [P, I32, I32, I32, I32, P, P]),
     "frcnn_reg2bbox": (I32, [P, P, I64, P, P]),
-    "frcnn_propose_workspace_size": (SZ, [ctypes.POINTER(ProposeParams)]),
+    "frcnn_rpn_head_epilogue": (I32, [P, P, I32, I32, I32, I32, P, P, P, P]),
+    "frcnn_propose_workspace_size":(SZ, [ctypes.POINTER(ProposeParams)]),
     "frcnn_propose": (I32, [ctypes.POINTER(ProposeParams), P, P, P, P, P, P, P, P, SZ, P]),
     "frcnn_nms_workspace_size": (SZ, [I64]),
     "frcnn_nms": (I32, [P, P, I64, F64, P, P, P, SZ, P]),

@@ -221,6 +221,51 @@ def propose(scores: torch.Tensor, deltas: torch.Tensor, *, img_w: float, img_h: 
     return rois, idx, cnt
 
 
+# ------------------------------------------------------------- RPN epilogue
+class _RPNHeadEpilogueFunction(torch.autograd.Function):
+    """nets/rpn.py:117-124 as one launch.  The backward of the two permutes is
+    the inverse permute (plain tensor ops); the fg scores feed only the
+    (non-differentiable) proposal layer, as in the reference."""
+
+    @staticmethod
+    def forward(ctx, cls, reg, K):
+        lib = _lib.load()
+        N, C2, H, W = cls.shape
+        if C2 != 2 * K or tuple(reg.shape) != (N, 4 * K, H, W):
+            raise RuntimeError(f"rpn_head_epilogue: cls {tuple(cls.shape)} / reg {tuple(reg.shape)} "
+                               f"do not match K={K}")
+        A = H * W * K
+        cls_nhwc = torch.empty((N, A, 2), dtype=torch.float32, device=cls.device)
+        fg = torch.empty((N, A), dtype=torch.float32, device=cls.device)
+        reg_nhwc = torch.empty((N, A, 4), dtype=torch.float32, device=cls.device)
+        _lib.check(lib.frcnn_rpn_head_epilogue(_lib.ptr(cls), _lib.ptr(reg), N, K, H, W,
+                                               _lib.ptr(cls_nhwc), _lib.ptr(fg), _lib.ptr(reg_nhwc),
+                                               _lib.stream_ptr()), "rpn_head_epilogue")
+        ctx.meta = (N, K, H, W)
+        ctx.mark_non_differentiable(fg)
+        return cls_nhwc, fg, reg_nhwc
+
+    @staticmethod
+    def backward(ctx, g_cls, _g_fg, g_reg):
+        N, K, H, W = ctx.meta
+        gc = gr = None
+        if g_cls is not None:
+            gc = g_cls.reshape(N, H, W, 2 * K).permute(0, 3, 1, 2).contiguous()
+        if g_reg is not None:
+            gr = g_reg.reshape(N, H, W, 4 * K).permute(0, 3, 1, 2).contiguous()
+        return gc, gr, None
+
+
+def rpn_head_epilogue(cls: torch.Tensor, reg: torch.Tensor, K: int):
+    """nets/rpn.py:117-124: conv outputs cls [N,2K,H,W], reg [N,4K,H,W] (device,
+    fp32) -> (cls_nhwc [N,A,2], fg [N,A], reg_nhwc [N,A,4]), A = H*W*K.
+    ``cls_nhwc.permute(0, 2, 1)`` is the reference's returned ``cls``; ``fg`` is
+    its ``cls_fg_softmax``; ``reg_nhwc`` its ``reg``."""
+    if cls.dim() != 4 or reg.dim() != 4:
+        raise RuntimeError("rpn_head_epilogue: cls and reg must be NCHW")
+    return _RPNHeadEpilogueFunction.apply(cls.float().contiguous(), reg.float().contiguous(), int(K))
+
+
 def roi_transform(rois: torch.Tensor, roi_inds: torch.Tensor, img_h, img_w, feat_h: int,
                   feat_w: int) -> torch.Tensor:
     """nets/heads.py:42-47 on device: [R,4] image rois + [R] inds -> [R,5]."""

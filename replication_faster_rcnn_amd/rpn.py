@@ -4,8 +4,9 @@
 call signatures and return types (nets/rpn.py:20-138).  The proposal layer is
 the batched HIP pipeline (``ops.propose``): the per-image Python loop of
 nets/rpn.py:131-136 becomes one launch sequence over the whole batch, with
-anchors generated inside the decode kernel.  The 3x3/1x1 convolutions and the
-softmax stay plain PyTorch (not the target).
+anchors generated inside the decode kernel.  The conv outputs' permutes and
+the fg softmax are one HIP launch (``ops.rpn_head_epilogue``); the 3x3/1x1
+convolutions stay plain PyTorch (not the target).
 """
 from __future__ import annotations
 
@@ -88,21 +89,19 @@ class RPN(nn.Module):
         """-> (cls [N,2,A], reg [N,A,4], rois [sum R,4], roi_inds fp32 [sum R], anchors [A,4])."""
         n_img, _, conv_h, conv_w = x.shape
         x = F.relu(self.conv1(x))
-        cls = self.cls(x)
-        cls = cls.permute(0, 2, 3, 1).contiguous().view(n_img, -1, 2)
-        cls_fg_softmax = F.softmax(cls, dim=-1)[:, :, 1].contiguous().view(n_img, -1)
-        cls = cls.permute(0, 2, 1)
-        reg = self.reg(x)
-        reg = reg.permute(0, 2, 3, 1).contiguous().view(n_img, -1, 4)
-
+        # nets/rpn.py:117-124: permute/contiguous/softmax/slice in ONE launch
+        # (ops.rpn_head_epilogue); results return to x's device like the reference's
         dev = _lib.device()
+        cls_nhwc, cls_fg_softmax, reg = ops.rpn_head_epilogue(
+            self.cls(x).to(dev), self.reg(x).to(dev), self.K)
+        cls = cls_nhwc.to(x.device).permute(0, 2, 1)
+
         if self._base_dev is None:
             self._base_dev = generate_anchor_base_device(ratios=self._ratios,
                                                          anchor_scales=self._scales)
         pl = self.proposal_layer
         rois_p, _, cnt = ops.propose(
-            cls_fg_softmax.detach().to(dev, torch.float32).contiguous(),
-            reg.detach().to(dev, torch.float32).contiguous(), img_w=img_width, img_h=img_height,
+            cls_fg_softmax, reg.detach(), img_w=img_width, img_h=img_height,
             pre_nms=pl.pre_nms, post_nms=pl.post_nms, nms_thresh=pl.nms_threshold,
             min_size=pl.min_size, anchor_base=self._base_dev, feat_h=conv_h, feat_w=conv_w,
             feat_stride=self.feat_stride)
@@ -116,4 +115,4 @@ class RPN(nn.Module):
         if self.anchors_as_numpy:
             anchors = anchors.cpu().numpy()
         self.anchors = anchors
-        return cls, reg, rois, roi_inds, anchors
+        return cls, reg.to(x.device), rois, roi_inds, anchors

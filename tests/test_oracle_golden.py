@@ -3,6 +3,7 @@ produced (tests/golden/make_golden.py).  CPU only."""
 import hashlib
 
 import numpy as np
+import torch
 import pytest
 
 from oracle import ref_numpy as orc
@@ -123,3 +124,19 @@ def test_targets_vs_reference(golden, tag):
         assert np.array_equal(np.random.get_state()[1], g["rng_key_out"])
     finally:
         np.random.set_state(saved)
+
+
+@pytest.mark.parametrize("K,H,W", [(9, 38, 38), (15, 7, 11)])
+def test_rpn_head_epilogue_oracle_vs_torch(K, H, W):
+    """Pins oracle.rpn_head_epilogue against the genuine torch ops the reference
+    runs at nets/rpn.py:117-124: permutes exact, fg softmax within 2 ulp-scale
+    relative error (torch's CPU exp is host-dependent in its last bits)."""
+    g = torch.Generator().manual_seed(K)
+    cls = torch.randn(2, 2 * K, H, W, generator=g) * 3
+    reg = torch.randn(2, 4 * K, H, W, generator=g)
+    c_t = cls.permute(0, 2, 3, 1).contiguous().view(2, -1, 2)
+    fg_t = torch.nn.functional.softmax(c_t, dim=-1)[:, :, 1].contiguous().view(2, -1)
+    r_t = reg.permute(0, 2, 3, 1).contiguous().view(2, -1, 4)
+    c, fg, r = orc.rpn_head_epilogue(cls.numpy(), reg.numpy())
+    assert np.array_equal(c, c_t.numpy()) and np.array_equal(r, r_t.numpy())
+    np.testing.assert_allclose(fg, fg_t.numpy(), rtol=1e-6, atol=1e-30)
