@@ -56,6 +56,14 @@ def parse():
                     help="with --streams 2 (inference configs): proposal layers of consecutive "
                          "steps round-robin over this many HIP streams, so step k+1's and "
                          "k+2's proposals (latency bound, few CUs busy) overlap each other too")
+    ap.add_argument("--prop-buffers", type=int, default=4,
+                    help="--issue capi: proposal output sets in flight (multiple of --prop-streams)")
+    ap.add_argument("--issue", default="ops", choices=("capi", "ops"),
+                    help="inference configs: ops = the Python drop-in ops (default); capi = "
+                         "each step is two direct C-ABI calls on preallocated buffers (a native "
+                         "host's issue path: 40 vs 88 us of host time per step, but the proposal "
+                         "chains then run ahead into the RoIPool and the step is slower, "
+                         "110 vs 99 us -- kept as an A/B)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-baseline sample (rank 0, N=1 only); 0 disables")
     return ap.parse_args()
@@ -225,6 +233,92 @@ def inference_step_fn(args, c, sc, de, x, base, world, ev):
     return step
 
 
+def inference_capi_fn(args, c, sc, de, x, base, world, ev):
+    """cfg1-4, issued straight through the C-ABI (include/frcnn_capi.h) the way
+    a native host would: parameters, device buffers and workspaces set up once,
+    so a step is two library calls plus stream events (~40 us of host time vs
+    ~88 us for the torch-op step, host_issue_us_per_step).  Measured (cfg2):
+    the faster issue lets proposal chains run ahead beside the RoIPool, which
+    then slows (90 vs 78 us) and the step is slower (110 vs 99 us) for 2, 4 or
+    8 buffer sets and 2-4 proposal streams, so --issue ops stays the default.
+    Same streams and overlap: step k's proposals on proposal stream k % P, its
+    RoIPool on the pool stream after them; a proposal buffer is rewritten only
+    after the pool that read it (event), so buffers are per proposal stream.
+    HIP graphs were measured as the alternative: a replay serialises the
+    captured branches and costs ~40 us of host time (126 us per step)."""
+    import ctypes
+    from replication_faster_rcnn_amd import _lib
+    from replication_faster_rcnn_amd import dist as fdist
+    lib = _lib.load()
+    N, dev = sc.size(0), sc.device
+    post = c["post_nms"]
+    Cc, H, W = x.shape[1:]
+    R = N * post
+    s_props, s_pool = make_streams(args, dev)
+    if not isinstance(s_props, list):
+        s_props = [s_props]
+    P = len(s_props)
+    B = max(P, args.prop_buffers)  # proposal output sets: run-ahead of B-1 steps
+    p = _lib.ProposeParams()
+    p.N, p.A, p.K = N, sc.size(1), base.size(0)
+    p.feat_h, p.feat_w, p.feat_stride = c["feat_h"], c["feat_w"], 16
+    p.img_h, p.img_w, p.min_size = float(c["img_h"]), float(c["img_w"]), 16.0
+    p.pre_nms, p.post_nms, p.iou_threshold = int(c["pre_nms"]), int(post), 0.7
+    pref = ctypes.byref(p)
+    ws_p = [_lib.workspace(lib.frcnn_propose_workspace_size(pref), dev) for _ in range(P)]
+    bufs = [(torch.zeros((N, post, 4), dtype=torch.float32, device=dev),
+             torch.full((N, post), -1, dtype=torch.int32, device=dev),
+             torch.zeros((N,), dtype=torch.int32, device=dev)) for _ in range(B)]
+    inds = torch.arange(N, device=dev, dtype=torch.float32).repeat_interleave(post)
+    out = torch.empty((R, Cc, 7, 7), dtype=torch.float32, device=dev)
+    am = torch.empty((R, Cc, 7, 7), dtype=torch.int32, device=dev)
+    boxes = torch.empty((R, 5), dtype=torch.float32, device=dev)
+    ws_r = _lib.workspace(lib.frcnn_roi_pool_fwd_workspace_size(R, N, Cc), dev)
+    V = ctypes.c_void_p
+    sp = [V(s.cuda_stream) for s in s_props]
+    spool = V(s_pool.cuda_stream)
+    prop_args = [(pref, V(sc.data_ptr()), V(de.data_ptr()), V(0), V(base.data_ptr()),
+                  V(b[0].data_ptr()), V(b[1].data_ptr()), V(b[2].data_ptr()),
+                  V(ws_p[i % P].data_ptr()), ws_p[i % P].numel(), sp[i % P])
+                 for i, b in enumerate(bufs)]
+    pool_args = [(V(x.data_ptr()), V(b[0].data_ptr()), V(inds.data_ptr()), R, N, Cc, H, W, 7, 7,
+                  float(c["img_h"]), float(c["img_w"]), 1.0, 1, V(boxes.data_ptr()),
+                  V(out.data_ptr()), V(am.data_ptr()), V(ws_r.data_ptr()), ws_r.numel(), spool)
+                 for b in bufs]
+    ready = [torch.cuda.Event() for _ in range(B)]
+    done = [None] * B
+    n_ev = args.steps + 1
+    tev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(n_ev)]
+    k = [0, 0]
+
+    def step(timed):
+        j = k[0] % B  # buffer set; stream k % P (B is a multiple of P)
+        s = s_props[k[0] % P]
+        k[0] += 1
+        if done[j] is not None:
+            s.wait_event(done[j])  # the pool that read bufs[j] last time
+        _lib.check(lib.frcnn_propose(*prop_args[j]), "propose")
+        if world > 1:  # the only collective: detections of all ranks (RCCL over xGMI)
+            with torch.cuda.stream(s):
+                fdist.all_gather_detections(*bufs[j])
+        ready[j].record(s)
+        s_pool.wait_event(ready[j])
+        if timed:
+            e0, e1 = tev[k[1] % n_ev]
+            k[1] += 1
+            e0.record(s_pool)
+        _lib.check(lib.frcnn_roi_pool_fwd_head(*pool_args[j]), "roi_pool_head")
+        if timed:
+            e1.record(s_pool)
+            ev["fwd"].append((e0, e1))
+        if done[j] is None:
+            done[j] = torch.cuda.Event()
+        done[j].record(s_pool)
+        return bufs[j][2]
+    return step
+
+
 def train_step_fn(args, c, sc, de, x, base, world, ev, first_image):
     """cfg5 (training step, train.py:59-127 minus the dense layers): propose
     (12000->600) -> anchor targets of every image -> proposal targets of every
@@ -290,6 +384,7 @@ def main():
     from replication_faster_rcnn_amd import anchors as A
     from replication_faster_rcnn_amd import dist as fdist
     train = args.config == "cfg5"
+    capi = args.issue == "capi" and not train
     per_rank = c_batch(args.config)
     mine = fdist.shard(per_rank * world, rank, world)  # weak scaling: per_rank images per GPU
     c, sc, de, x = make_inputs(args.config, len(mine), mine.start, dev)
@@ -299,7 +394,7 @@ def main():
     if train:
         step = train_step_fn(args, c, sc, de, x, base, world, ev, mine.start)
     else:
-        step = inference_step_fn(args, c, sc, de, x, base, world, ev)
+        step = (inference_capi_fn if capi else inference_step_fn)(args, c, sc, de, x, base, world, ev)
 
     for _ in range(args.warmup):
         cnt = step(False)
@@ -310,6 +405,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         cnt = step(True)
+    t_issue = time.perf_counter() - t0  # host time to enqueue the K steps
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -351,12 +447,14 @@ def main():
         "config": {"workload": workload, "global_batch": world * N,
                    "parallelism": f"dp{world} (per-image sharding)", "streams": args.streams,
                    "prop_streams": args.prop_streams if (args.streams == 2 and not train) else 1,
+                   "issue": "capi" if capi else "ops",
                    "prop_cus": args.prop_cus if args.streams == 2 else 0},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "roi_pool_bwd_kernel" if train else "roi_pool_fwd_px8q_kernel<head>",
                      "kernel_us": dom_ms * 1e3, "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": None,
+        "host_issue_us_per_step": t_issue / args.steps * 1e6,
     }
     if train:
         rec["roofline"]["fwd_us"] = fwd_ms * 1e3

@@ -189,7 +189,7 @@ def roi_pool(input: torch.Tensor, boxes, output_size, spatial_scale: float = 1.0
 def propose(scores: torch.Tensor, deltas: torch.Tensor, *, img_w: float, img_h: float,
             pre_nms: int, post_nms: int, nms_thresh: float = 0.7, min_size: float = 16,
             anchors: torch.Tensor = None, anchor_base: torch.Tensor = None, feat_h: int = 0,
-            feat_w: int = 0, feat_stride: int = 16):
+            feat_w: int = 0, feat_stride: int = 16, out=None, workspace=None):
     """Batched proposal layer on device tensors.
 
     scores fp32 [N, A], deltas fp32 [N, A, 4]; either explicit ``anchors``
@@ -210,10 +210,20 @@ def propose(scores: torch.Tensor, deltas: torch.Tensor, *, img_w: float, img_h: 
     p.K, p.feat_h, p.feat_w, p.feat_stride = K, feat_h, feat_w, feat_stride
     p.img_h, p.img_w, p.min_size = float(img_h), float(img_w), float(min_size)
     p.pre_nms, p.post_nms, p.iou_threshold = int(pre_nms), int(post_nms), float(nms_thresh)
-    rois = torch.empty((N, post_nms, 4), dtype=torch.float32, device=dev)
-    idx = torch.empty((N, post_nms), dtype=torch.int32, device=dev)
-    cnt = torch.empty((N,), dtype=torch.int32, device=dev)
-    ws = _lib.workspace(lib.frcnn_propose_workspace_size(p), dev)
+    if out is None:
+        rois = torch.empty((N, post_nms, 4), dtype=torch.float32, device=dev)
+        idx = torch.empty((N, post_nms), dtype=torch.int32, device=dev)
+        cnt = torch.empty((N,), dtype=torch.int32, device=dev)
+    else:  # caller-owned outputs (static buffers of a captured HIP graph)
+        rois, idx, cnt = out
+        if (tuple(rois.shape) != (N, post_nms, 4) or tuple(idx.shape) != (N, post_nms)
+                or tuple(cnt.shape) != (N,) or rois.dtype != torch.float32
+                or idx.dtype != torch.int32 or cnt.dtype != torch.int32):
+            raise RuntimeError("propose: out buffers must be fp32 [N,post,4], int32 [N,post], int32 [N]")
+    need = lib.frcnn_propose_workspace_size(p)
+    ws = workspace if workspace is not None else _lib.workspace(need, dev)
+    if ws.numel() < need:
+        raise RuntimeError(f"propose: workspace of {ws.numel()} B < {need} B")
     _lib.check(lib.frcnn_propose(p, _lib.ptr(scores), _lib.ptr(deltas), _lib.ptr(anchors),
                                  _lib.ptr(anchor_base), _lib.ptr(rois), _lib.ptr(idx),
                                  _lib.ptr(cnt), _lib.ptr(ws), ws.numel(), _lib.stream_ptr()),

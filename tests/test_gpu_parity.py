@@ -495,3 +495,23 @@ def test_roi_pool_bwd_denormal_and_colliding_grads():
     gi = _roi_pool_bwd(torch.from_numpy(g).to(DEV), rois, am, x.shape, 1.0)
     ref = orc.roi_pool_backward(g, rois.cpu().numpy(), am.cpu().numpy(), x.shape)
     assert np.array_equal(gi.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+def test_propose_caller_buffers():
+    """ops.propose(out=..., workspace=...) writes the same result into caller-owned
+    buffers (the static-buffer path of bench.py --issue capi and of graph capture)."""
+    A = 38 * 63 * 9
+    sc = torch.from_numpy(np.stack([synth.rpn_scores(A, 3, i) for i in range(3)])).cuda()
+    de = torch.from_numpy(np.stack([synth.rpn_deltas(A, 3, i) for i in range(3)])).cuda()
+    base = A.generate_anchor_base_device()
+    kw = dict(img_w=1000, img_h=600, pre_nms=6000, post_nms=300, anchor_base=base, feat_h=38,
+              feat_w=63)
+    r0, i0, c0 = ops.propose(sc, de, **kw)
+    out = (torch.full_like(r0, 7.0), torch.full_like(i0, 5), torch.full_like(c0, 9))
+    ws = torch.empty(1 << 26, dtype=torch.uint8, device="cuda")
+    r1, i1, c1 = ops.propose(sc, de, out=out, workspace=ws, **kw)
+    assert r1.data_ptr() == out[0].data_ptr()
+    assert torch.equal(r0, r1) and torch.equal(i0, i1) and torch.equal(c0, c1)
+    with pytest.raises(RuntimeError):
+        ops.propose(sc, de, out=(out[0][:, :10], out[1], out[2]), **kw)
+
