@@ -500,9 +500,9 @@ def test_roi_pool_bwd_denormal_and_colliding_grads():
 def test_propose_caller_buffers():
     """ops.propose(out=..., workspace=...) writes the same result into caller-owned
     buffers (the static-buffer path of bench.py --issue capi and of graph capture)."""
-    A = 38 * 63 * 9
-    sc = torch.from_numpy(np.stack([synth.rpn_scores(A, 3, i) for i in range(3)])).cuda()
-    de = torch.from_numpy(np.stack([synth.rpn_deltas(A, 3, i) for i in range(3)])).cuda()
+    na = 38 * 63 * 9
+    sc = torch.from_numpy(np.stack([synth.rpn_scores(na, 3, i) for i in range(3)])).cuda()
+    de = torch.from_numpy(np.stack([synth.rpn_deltas(na, 3, i) for i in range(3)])).cuda()
     base = A.generate_anchor_base_device()
     kw = dict(img_w=1000, img_h=600, pre_nms=6000, post_nms=300, anchor_base=base, feat_h=38,
               feat_w=63)
