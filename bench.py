@@ -58,6 +58,11 @@ def parse():
                          "k+2's proposals (latency bound, few CUs busy) overlap each other too")
     ap.add_argument("--prop-buffers", type=int, default=4,
                     help="--issue capi: proposal output sets in flight (multiple of --prop-streams)")
+    ap.add_argument("--host-io", type=int, default=0, choices=(0, 1),
+                    help="1: PCIe-inclusive variant -- each step copies its inputs (scores, "
+                         "deltas, features) from pinned host memory and the rois + pooled "
+                         "features back, like the reference's host-resident tensors (never the "
+                         "default value)")
     ap.add_argument("--issue", default="ops", choices=("capi", "ops"),
                     help="inference configs: ops = the Python drop-in ops (default); capi = "
                          "each step is two direct C-ABI calls on preallocated buffers (a native "
@@ -205,16 +210,32 @@ def inference_step_fn(args, c, sc, de, x, base, world, ev):
     if not isinstance(s_props, list):
         s_props = [s_props]
     k_step = [0]
+    if args.host_io:  # reference-style host tensors: inputs H2D, rois + pooled D2H per step
+        h_in = [t.cpu().pin_memory() for t in (sc, de, x)]
+        d_in = [[torch.empty_like(t) for t in (sc, de, x)] for _ in s_props]
+        h_rois = torch.empty((N, post, 4), dtype=torch.float32).pin_memory()
+        h_pool = torch.empty((N * post, x.size(1), 7, 7), dtype=torch.float32).pin_memory()
+        done = [None] * len(s_props)
 
     def step(timed):
-        s_prop = s_props[k_step[0] % len(s_props)]
+        j = k_step[0] % len(s_props)
+        s_prop = s_props[j]
         k_step[0] += 1
         with torch.cuda.stream(s_prop):
-            rois, idx, cnt = ops.propose(sc, de, img_w=c["img_w"], img_h=c["img_h"],
+            sc_, de_, x_ = sc, de, x
+            if args.host_io:
+                if done[j] is not None:
+                    s_prop.wait_event(done[j])  # the pool that read d_in[j] last time
+                for d, h in zip(d_in[j], h_in):
+                    d.copy_(h, non_blocking=True)
+                sc_, de_, x_ = d_in[j]
+            rois, idx, cnt = ops.propose(sc_, de_, img_w=c["img_w"], img_h=c["img_h"],
                                          pre_nms=c["pre_nms"], post_nms=post, anchor_base=base,
                                          feat_h=c["feat_h"], feat_w=c["feat_w"])
             if world > 1:  # the only collective: detections of all ranks (RCCL over xGMI)
                 fdist.all_gather_detections(rois, idx, cnt)
+            if args.host_io:
+                h_rois.copy_(rois, non_blocking=True)
             ready = torch.cuda.Event()
             ready.record(s_prop)
         with torch.cuda.stream(s_pool):
@@ -224,11 +245,15 @@ def inference_step_fn(args, c, sc, de, x, base, world, ev):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s_pool)
             # ResnetHead's transform + pack + roi_pool (nets/heads.py:42-48): one launch
-            pooled, am, boxes = ops.roi_pool_head(x, rois.view(-1, 4), inds, 7, c["img_h"], c["img_w"],
+            pooled, am, boxes = ops.roi_pool_head(x_, rois.view(-1, 4), inds, 7, c["img_h"], c["img_w"],
                                                   rois_sorted=True)
             if timed:
                 e1.record(s_pool)
                 ev["fwd"].append((e0, e1))
+            if args.host_io:
+                h_pool.copy_(pooled, non_blocking=True)
+                done[j] = torch.cuda.Event()
+                done[j].record(s_pool)
         return cnt
     return step
 
@@ -385,6 +410,8 @@ def main():
     from replication_faster_rcnn_amd import dist as fdist
     train = args.config == "cfg5"
     capi = args.issue == "capi" and not train
+    if args.host_io and (capi or train):
+        raise SystemExit("--host-io is measured on the inference ops path only")
     per_rank = c_batch(args.config)
     mine = fdist.shard(per_rank * world, rank, world)  # weak scaling: per_rank images per GPU
     c, sc, de, x = make_inputs(args.config, len(mine), mine.start, dev)
@@ -448,6 +475,7 @@ def main():
                    "parallelism": f"dp{world} (per-image sharding)", "streams": args.streams,
                    "prop_streams": args.prop_streams if (args.streams == 2 and not train) else 1,
                    "issue": "capi" if capi else "ops",
+                   "host_io": bool(args.host_io),
                    "prop_cus": args.prop_cus if args.streams == 2 else 0},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
