@@ -196,3 +196,34 @@ def test_device_resident_rng_stream(rng_guard):
     st = np.random.get_state()
     np.random.seed(999)
     assert np.array_equal(np.random.get_state()[1], st[1])
+
+
+def test_anchor_targets_from_voc_annotations(rng_guard):
+    """utils/data_loader.py's gt format (data.load_targets + collate) straight into the
+    batched anchor targets: rows with label -1 (padding, difficult, the single-object
+    quirk) are dropped exactly as train.py:74-76 does, RNG stream kept."""
+    from replication_faster_rcnn_amd import data
+
+    def obj(name, y0, x0, y1, x1, dif="0"):
+        return (f"<object><name>{name}</name><difficult>{dif}</difficult><bndbox><xmin>{x0}</xmin>"
+                f"<ymin>{y0}</ymin><xmax>{x1}</xmax><ymax>{y1}</ymax></bndbox></object>")
+
+    xmls = ["<annotation>" + obj("dog", 40, 60, 200, 300) + obj("person", 100, 20, 370, 180)
+            + obj("car", 10, 10, 60, 90, dif="1") + obj("cat", 150.5, 250.5, 330, 480)
+            + "</annotation>",
+            "<annotation>" + obj("bird", 30, 30, 120, 160) + "</annotation>"]   # single object
+    samples = [data.load_targets(t, (375, 500)) for t in xmls]
+    boxes, labels = data.collate_targets(samples)
+    boxes, labels = boxes.numpy(), labels.numpy()
+    assert (labels[0] != -1).sum() == 3 and (labels[1] != -1).sum() == 0
+    anchors = orc.generate_anchors(orc.generate_anchor_base(), 16, 38, 38)
+    np.random.seed(11)
+    reg, lab = targets.anchor_targets(boxes, labels, anchors)
+    st = np.random.get_state()
+    np.random.seed(11)
+    for i in range(2):
+        v = labels[i] != -1
+        oreg, olab = orc.anchor_target(boxes[i, v], anchors)
+        assert np.array_equal(lab[i].cpu().numpy(), olab)
+        np.testing.assert_allclose(reg[i].cpu().numpy(), oreg, rtol=1e-12, atol=0)
+    assert np.array_equal(np.random.get_state()[1], st[1]) and np.random.get_state()[2] == st[2]
