@@ -35,13 +35,18 @@ const char* frcnn_version(void);
 const char* frcnn_last_error(void);
 
 /* Runtime helpers (no reference counterpart: the reference runs one image at
- * a time on the host).  CU count of the current device, and HIP streams
- * restricted to a CU subset (bit i of cu_mask = CU i, n_words 32-bit words) so
- * that the proposal layer and the RoIPool of consecutive steps can share the
- * chip by partition.  Destroy with frcnn_stream_destroy. */
+ * a time on the host).  CU count of the current device (sizes the grids). */
 int frcnn_device_cu_count(int* out);
-int frcnn_stream_create_cu_masked(const uint32_t* cu_mask, int n_words, void** stream);
-int frcnn_stream_destroy(void* stream);
+
+/* Kernel-path selection, process-global (tests and A/B tools; the default
+ * "auto" is what every caller should use).  op / path:
+ *   "roi_pool_fwd"   : "auto" | "dense" (image tile in LDS) | "generic" (one workgroup per RoI)
+ *   "roi_pool_bwd"   : "auto" | "ring" (latency-hidden plane owner) | "plain"
+ *   "propose"        : "auto" | "hybrid" | "lazy" (fused per image) | "wide" (chip-wide bitmask)
+ *   "roi_pool_split" : "auto" | "1".."64" (RoI shares per image and channel group)
+ * All paths give bit-identical results.  Not thread-safe against calls in
+ * flight on other threads; set it before launching. */
+int frcnn_set_path(const char* op, const char* path);
 
 /* ---------------------------------------------------------------- anchors */
 

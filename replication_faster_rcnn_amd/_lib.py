@@ -11,6 +11,7 @@ usable directly.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -40,8 +41,7 @@ SIGNATURES = {
     "frcnn_version": (ctypes.c_char_p, []),
     "frcnn_last_error": (ctypes.c_char_p, []),
     "frcnn_device_cu_count": (I32, [P]),
-    "frcnn_stream_create_cu_masked": (I32, [P, I32, P]),
-    "frcnn_stream_destroy": (I32, [P]),
+    "frcnn_set_path": (I32, [ctypes.c_char_p, ctypes.c_char_p]),
     "frcnn_anchor_base": (I32, [P, I32, P, I32, F64, P, P]),
     "frcnn_generate_anchors": (I32, [P, I32, I32, I32, I32, P, P]),
     "frcnn_reg2bbox": (I32, [P, P, I64, P, P]),
@@ -68,6 +68,7 @@ SIGNATURES = {
 }
 
 _lib = None
+_gpu_checked = False
 
 
 class FrcnnError(RuntimeError):
@@ -88,9 +89,12 @@ def load(require_gpu: bool = True):
             fn.restype = res
             fn.argtypes = args
         _lib = lib
-    if require_gpu and not torch.cuda.is_available():
-        raise FrcnnError("replication_faster_rcnn_amd needs an MI355X (no HIP device visible); "
-                         "there is no CPU fallback")
+    global _gpu_checked
+    if require_gpu and not _gpu_checked:
+        if not torch.cuda.is_available():
+            raise FrcnnError("replication_faster_rcnn_amd needs an MI355X (no HIP device visible); "
+                             "there is no CPU fallback")
+        _gpu_checked = True
     return _lib
 
 
@@ -117,6 +121,23 @@ def workspace(nbytes: int, dev) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
 
 
+_ws_cache = {}
+
+
+def cached_workspace(tag: str, nbytes: int, dev) -> torch.Tensor:
+    """Grow-only scratch buffer per (op, device, current stream): the C-ABI's
+    workspaces are stream-ordered scratch, so one buffer per stream serves every
+    call on that stream (no allocation on the issue path).  Allocated while the
+    stream is current, so the caching allocator orders its reuse on that stream."""
+    s = torch.cuda.current_stream(dev)
+    key = (tag, s.device_index, s.cuda_stream)
+    ws = _ws_cache.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
+        _ws_cache[key] = ws
+    return ws
+
+
 def cu_count() -> int:
     lib = load()
     n = ctypes.c_int(0)
@@ -124,15 +145,17 @@ def cu_count() -> int:
     return int(n.value)
 
 
-def cu_masked_stream(cus, device=None):
-    """A torch stream (ExternalStream) whose kernels run only on the given CU
-    indices (hipExtStreamCreateWithCUMask).  The HIP stream lives as long as
-    the process (streams are few and long-lived)."""
-    lib = load()
-    n_words = (max(cus) // 32 + 1) if cus else 1
-    mask = (ctypes.c_uint32 * n_words)()
-    for c in cus:
-        mask[c // 32] |= 1 << (c % 32)
-    h = ctypes.c_void_p(0)
-    check(lib.frcnn_stream_create_cu_masked(mask, n_words, ctypes.byref(h)), "stream_create_cu_masked")
-    return torch.cuda.ExternalStream(h.value, device=device)
+def set_path(op: str, path) -> None:
+    """frcnn_set_path: select a kernel path ("auto" restores the default)."""
+    lib = load(require_gpu=False)
+    check(lib.frcnn_set_path(op.encode(), str(path).encode()), f"set_path({op}, {path})")
+
+
+@contextlib.contextmanager
+def kernel_path(op: str, path):
+    """Run a block with one op's kernel path forced (tests / A-B tools)."""
+    set_path(op, path)
+    try:
+        yield
+    finally:
+        set_path(op, "auto")

@@ -1,9 +1,10 @@
 // C-ABI housekeeping: version string and the per-thread last-error message.
-#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 
@@ -27,15 +28,62 @@ int check_launch(const char* what) {
     return FRCNN_OK;
 }
 
+static PathCfg g_path;
+
+const PathCfg& path_cfg() { return g_path; }
+
+int device_cu_count() {
+    static int cus = 0;
+    if (cus <= 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+            cus = n;
+        else
+            cus = 256;
+    }
+    return cus;
+}
+
 }  // namespace frcnn
 
-extern "C" const char* frcnn_version(void) { return "frcnn_mi355x 0.1.0 gfx950"; }
+extern "C" const char* frcnn_version(void) { return "frcnn_mi355x 0.2.0 gfx950"; }
+
+extern "C" int frcnn_set_path(const char* op, const char* path) {
+    using namespace frcnn;
+    if (!op || !path) {
+        set_error("frcnn_set_path: null argument");
+        return FRCNN_EINVAL;
+    }
+    auto is = [&](const char* a, const char* b) { return std::strcmp(a, b) == 0; };
+    const bool aut = is(path, "auto");
+    if (is(op, "roi_pool_fwd") && (aut || is(path, "dense") || is(path, "generic"))) {
+        g_path.roi_fwd = is(path, "generic") ? kPathGeneric : kPathAuto;
+    } else if (is(op, "roi_pool_bwd") && (aut || is(path, "ring") || is(path, "plain"))) {
+        g_path.roi_bwd = is(path, "plain") ? kPathPlain : kPathAuto;
+    } else if (is(op, "propose") &&
+               (aut || is(path, "hybrid") || is(path, "lazy") || is(path, "wide"))) {
+        g_path.propose = aut ? kPathAuto : is(path, "hybrid") ? kPathHybrid
+                                         : is(path, "lazy")   ? kPathLazy
+                                                              : kPathWide;
+    } else if (is(op, "roi_pool_split")) {
+        char* end = nullptr;
+        const long v = aut ? 0 : std::strtol(path, &end, 10);
+        if (!aut && (end == path || *end != '\0' || v < 0 || v > 64)) {
+            set_error("frcnn_set_path: roi_pool_split must be auto or 0..64, got '%s'", path);
+            return FRCNN_EINVAL;
+        }
+        g_path.roi_split = static_cast<int>(v);
+    } else {
+        set_error("frcnn_set_path: unknown op / path '%s' / '%s'", op, path);
+        return FRCNN_EINVAL;
+    }
+    return FRCNN_OK;
+}
 
 extern "C" const char* frcnn_last_error(void) { return frcnn::g_err; }
 
-// Streams restricted to a set of CUs (hipExtStreamCreateWithCUMask): lets the
-// latency-bound proposal layer keep a few CUs of its own while the RoIPool of
-// the previous step fills the rest, instead of waiting for whole CUs to drain.
+// CU count of the current device, for callers sizing their own launches.
 extern "C" int frcnn_device_cu_count(int* out) {
     int dev = 0, n = 0;
     if (!out) {
@@ -46,26 +94,5 @@ extern "C" int frcnn_device_cu_count(int* out) {
         hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return frcnn::check_launch("frcnn_device_cu_count");
     *out = n;
-    return FRCNN_OK;
-}
-
-extern "C" int frcnn_stream_create_cu_masked(const uint32_t* cu_mask, int n_words, void** stream) {
-    if (!cu_mask || n_words <= 0 || !stream) {
-        frcnn::set_error("frcnn_stream_create_cu_masked: bad argument");
-        return FRCNN_EINVAL;
-    }
-    hipStream_t s = nullptr;
-    if (hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(n_words), cu_mask) != hipSuccess) {
-        (void)hipGetLastError();
-        frcnn::set_error("frcnn_stream_create_cu_masked: hipExtStreamCreateWithCUMask failed");
-        return FRCNN_EHIP;
-    }
-    *stream = s;
-    return FRCNN_OK;
-}
-
-extern "C" int frcnn_stream_destroy(void* stream) {
-    if (stream && hipStreamDestroy(static_cast<hipStream_t>(stream)) != hipSuccess)
-        return frcnn::check_launch("frcnn_stream_destroy");
     return FRCNN_OK;
 }

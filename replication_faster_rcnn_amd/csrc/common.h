@@ -13,6 +13,25 @@ namespace frcnn {
 
 void set_error(const char* fmt, ...);
 
+// Kernel-path selection (frcnn_set_path; process-global, default "auto").
+// Read once per call as plain ints: no getenv on the launch path.
+constexpr int kPathAuto = 0;
+constexpr int kPathGeneric = 1;  // roi_pool_fwd: one workgroup per RoI
+constexpr int kPathPlain = 1;    // roi_pool_bwd: the unpipelined plane-owner kernel
+constexpr int kPathHybrid = 1;   // propose: fused per image + chip-wide first-chunk mask
+constexpr int kPathLazy = 2;     // propose: fused per image, lazy NMS from the first chunk on
+constexpr int kPathWide = 3;     // propose: chip-wide sort + bitmask NMS
+struct PathCfg {
+    int roi_fwd = kPathAuto;
+    int roi_bwd = kPathAuto;
+    int propose = kPathAuto;
+    int roi_split = 0;  // RoI shares per (image, channel group); 0 = auto
+};
+const PathCfg& path_cfg();
+
+// CU count of the current device (cached after the first call).
+int device_cu_count();
+
 // Launch-and-check helper used by every C-ABI wrapper: returns FRCNN_EHIP
 // with the HIP message when the last launch failed.
 int check_launch(const char* what);

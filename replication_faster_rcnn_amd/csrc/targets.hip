@@ -268,17 +268,12 @@ __device__ __forceinline__ uint32_t mask_for(uint32_t v) {
 // step; starting from "all accepted", the iteration accept <- f(prefix(accept))
 // reaches the unique fixed point (word t depends only on words < t) in a few
 // rounds, since a rejection shifts later steps by one and only flips words
-// near a bound.  Measured per block (tools/probe_sampler.py): 16 waves with a
+// near a bound.  Measured per block (round-1 timeline probe, tools/experiments): 16 waves with a
 // barrier per round ~4 us, one wave alone ~2.6-3.3 us (issue bound), 4 waves.
 constexpr int kSampThreads = 256;
 constexpr int kSampWaves = kSampThreads / 64;  // 4: one per SIMD
 constexpr int kWpl = 3;                        // words per lane
 constexpr int kSeg = kWpl * 64;                // words per wave segment (4 x 192 >= 624)
-// tools-only timeline probe of the sampler (tools/probe_sampler.py): per
-// 624-word block [start, after twist, after automaton, rounds]
-__device__ int g_samp_probe_on;
-__device__ int g_samp_probe_n;
-__device__ unsigned long long g_samp_probe[4 * 2048];
 
 struct StreamLds {
     uint32_t key[kMtN];
@@ -326,13 +321,10 @@ __device__ void fy_steps_block(StreamLds& S, int i_hi, int i_lo, int rec_lo, int
     int i_cur = i_hi;
     int it = 0;  // round counter: round r writes tot[r % 3], reads tot[(r + 2) % 3]
     while (i_cur >= i_lo) {  // block-uniform: every thread tracks the same i_cur
-        const bool probe = g_samp_probe_on != 0;
-        unsigned long long pt0 = probe ? __builtin_amdgcn_s_memrealtime() : 0ull, pt1 = pt0;
         if (S.pos == kMtN) {
             mt_twist_block(S);
             if (tid == 0) S.pos = 0;
             __syncthreads();
-            if (probe) pt1 = __builtin_amdgcn_s_memrealtime();
         }
         const int pos = S.pos;
         const int cnt = kMtN - pos;
@@ -357,9 +349,8 @@ __device__ void fy_steps_block(StreamLds& S, int i_hi, int i_lo, int rec_lo, int
         int il[kWpl];
         uint32_t m[kWpl];
         bool a[kWpl];
-        int total = 0, rounds = 0;
+        int total = 0;
         for (;;) {
-            ++rounds;
             for (;;) {  // this segment, exact for the assumed `base`
                 int b = base;
 #pragma unroll
@@ -414,16 +405,6 @@ __device__ void fy_steps_block(StreamLds& S, int i_hi, int i_lo, int rec_lo, int
             consumed = max(max(l4.x, l4.y), max(l4.z, l4.w));
         }
         i_cur -= total;
-        if (probe && tid == 0) {
-            const int slot = g_samp_probe_n;
-            if (slot < 2048) {
-                g_samp_probe[4 * slot + 0] = pt0;
-                g_samp_probe[4 * slot + 1] = pt1;
-                g_samp_probe[4 * slot + 2] = __builtin_amdgcn_s_memrealtime();
-                g_samp_probe[4 * slot + 3] = static_cast<unsigned long long>(rounds);
-                g_samp_probe_n = slot + 1;
-            }
-        }
         __syncthreads();  // everyone has read S.pos / S.last / the totals
         if (tid == 0) S.pos = pos + consumed;
         __syncthreads();
@@ -1010,18 +991,3 @@ extern "C" int frcnn_bbox2reg(const void* anchors, int a_is_f64, const void* bbo
     return FRCNN_OK;
 }
 
-// tools-only (not part of the C-ABI): sampler timeline probe
-extern "C" int frcnn_dbg_samp_probe(int on, unsigned long long* host, int n) {
-    if (host) {
-        if (n > 4 * 2048) n = 4 * 2048;
-        if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_samp_probe), sizeof(unsigned long long) * n) != hipSuccess)
-            return -2;
-        int cnt = 0;
-        if (hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(g_samp_probe_n), sizeof(int)) != hipSuccess) return -2;
-        return cnt;
-    }
-    const int zero = 0;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_samp_probe_n), &zero, sizeof(int)) != hipSuccess) return -2;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_samp_probe_on), &on, sizeof(int)) != hipSuccess) return -2;
-    return 0;
-}

@@ -23,19 +23,24 @@ class ResnetHead(nn.Module):
         self.roi_size = roi_size
         self.spatial_scale = spatial_scale
 
-    def forward(self, x, rois, roi_inds, img_h, img_w):
-        """-> (cls [N, n_classes, n_sample], reg [N, n_sample, n_classes*4])."""
+    def forward(self, x, rois, roi_inds, img_h, img_w, rois_sorted=None):
+        """-> (cls [N, n_classes, n_sample], reg [N, n_sample, n_classes*4]).
+
+        ``rois_sorted`` (extension): True promises RoIs grouped by non-decreasing
+        image index, as RPN.forward (nets/rpn.py:129-136) and train.py's sampler
+        loop (:91-108) produce them -- the one-launch path.  None checks: on the
+        host for host-resident indices (the reference's case, no device sync),
+        with one device->host sync for device-resident ones."""
         N = x.shape[0]
         dev = _lib.device()
+        if rois_sorted is None:
+            bi = torch.as_tensor(roi_inds).detach().to(torch.int64)  # host tensors: no sync
+            rois_sorted = bool((bi[1:] >= bi[:-1]).all()) if bi.numel() > 1 else True
         r = torch.as_tensor(rois).detach().to(dev, torch.float32).contiguous()
         ri = torch.as_tensor(roi_inds).detach().to(dev, torch.float32).contiguous()
-        # RPN.forward (nets/rpn.py:129-136) and train.py's sampler loop group the
-        # RoIs by image; the one-launch path relies on that, so check it.
-        bi = ri.to(torch.int32)
-        sorted_inds = bool((bi[1:] >= bi[:-1]).all()) if bi.numel() > 1 else True
         out_dev = x.device
         cropped = ops.roi_pool_head(x, r, ri, (self.roi_size, self.roi_size), img_h, img_w,
-                                    self.spatial_scale, rois_sorted=sorted_inds)[0].to(out_dev)
+                                    self.spatial_scale, rois_sorted=bool(rois_sorted))[0].to(out_dev)
         fc6 = self.classifier(cropped)
         fc6 = fc6.view(fc6.shape[0], -1)
         reg = self.reg(fc6)

@@ -23,6 +23,8 @@ from . import _lib
 
 
 def _to_dev(t: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
+    if t.is_cuda and t.dtype == dtype and t.is_contiguous():  # the device-resident fast path
+        return t
     return t.to(device=_lib.device(), dtype=dtype).contiguous()
 
 
@@ -55,7 +57,7 @@ def _roi_pool_fwd(x: torch.Tensor, rois: torch.Tensor, ph: int, pw: int, ss: flo
     R = rois.size(0)
     out = torch.empty((R, C, ph, pw), dtype=torch.float32, device=x.device)
     am = torch.empty((R, C, ph, pw), dtype=torch.int32, device=x.device)
-    ws = _lib.workspace(lib.frcnn_roi_pool_fwd_workspace_size(R, N, C), x.device)
+    ws = _lib.cached_workspace("roi_pool_fwd", lib.frcnn_roi_pool_fwd_workspace_size(R, N, C), x.device)
     _lib.check(lib.frcnn_roi_pool_fwd(_lib.ptr(x), _lib.ptr(rois), R, N, C, H, W, ph, pw, float(ss),
                                       int(bool(rois_sorted)), _lib.ptr(out), _lib.ptr(am),
                                       _lib.ptr(ws), ws.numel(), _lib.stream_ptr()), "roi_pool forward")
@@ -77,7 +79,8 @@ def _roi_pool_bwd(grad: torch.Tensor, rois: torch.Tensor, am: torch.Tensor, shap
     N, C, H, W = shape
     R, _, ph, pw = grad.shape
     gi = torch.empty((N, C, H, W), dtype=torch.float32, device=grad.device)
-    ws = _lib.workspace(lib.frcnn_roi_pool_bwd_workspace_size(R, N, ph, pw), grad.device)
+    ws = _lib.cached_workspace("roi_pool_bwd", lib.frcnn_roi_pool_bwd_workspace_size(R, N, ph, pw),
+                               grad.device)
     _lib.check(lib.frcnn_roi_pool_bwd(_lib.ptr(grad), _lib.ptr(rois), _lib.ptr(am), R, N, C, H, W,
                                       ph, pw, float(ss), _lib.ptr(gi), _lib.ptr(ws), ws.numel(),
                                       _lib.stream_ptr()), "roi_pool backward")
@@ -101,23 +104,28 @@ class _RoIPoolFunction(torch.autograd.Function):
         return gi, None, None, None, None, None
 
 
+def _roi_pool_head_fwd(x, rois, roi_inds, ph, pw, img_h, img_w, ss, rois_sorted):
+    lib = _lib.load()
+    N, C, H, W = x.shape
+    R = rois.size(0)
+    boxes = torch.empty((R, 5), dtype=torch.float32, device=x.device)
+    out = torch.empty((R, C, ph, pw), dtype=torch.float32, device=x.device)
+    am = torch.empty((R, C, ph, pw), dtype=torch.int32, device=x.device)
+    ws = _lib.cached_workspace("roi_pool_fwd", lib.frcnn_roi_pool_fwd_workspace_size(R, N, C), x.device)
+    _lib.check(lib.frcnn_roi_pool_fwd_head(
+        _lib.ptr(x), _lib.ptr(rois), _lib.ptr(roi_inds), R, N, C, H, W, ph, pw, float(img_h),
+        float(img_w), float(ss), int(bool(rois_sorted)), _lib.ptr(boxes), _lib.ptr(out),
+        _lib.ptr(am), _lib.ptr(ws), ws.numel(), _lib.stream_ptr()), "roi_pool_head forward")
+    return out, am, boxes
+
+
 class _RoIPoolHeadFunction(torch.autograd.Function):
     """nets/heads.py:42-48 (RoI transform + pack + roi_pool) as one op; the
     backward is roi_pool's, on the [R,5] boxes the forward wrote."""
 
     @staticmethod
     def forward(ctx, x, rois, roi_inds, ph, pw, img_h, img_w, ss, rois_sorted):
-        lib = _lib.load()
-        N, C, H, W = x.shape
-        R = rois.size(0)
-        boxes = torch.empty((R, 5), dtype=torch.float32, device=x.device)
-        out = torch.empty((R, C, ph, pw), dtype=torch.float32, device=x.device)
-        am = torch.empty((R, C, ph, pw), dtype=torch.int32, device=x.device)
-        ws = _lib.workspace(lib.frcnn_roi_pool_fwd_workspace_size(R, N, C), x.device)
-        _lib.check(lib.frcnn_roi_pool_fwd_head(
-            _lib.ptr(x), _lib.ptr(rois), _lib.ptr(roi_inds), R, N, C, H, W, ph, pw, float(img_h),
-            float(img_w), float(ss), int(bool(rois_sorted)), _lib.ptr(boxes), _lib.ptr(out),
-            _lib.ptr(am), _lib.ptr(ws), ws.numel(), _lib.stream_ptr()), "roi_pool_head forward")
+        out, am, boxes = _roi_pool_head_fwd(x, rois, roi_inds, ph, pw, img_h, img_w, ss, rois_sorted)
         ctx.save_for_backward(boxes, am)
         ctx.meta = (tuple(x.shape), ss)
         ctx.mark_non_differentiable(am, boxes)
@@ -146,8 +154,11 @@ def roi_pool_head(input: torch.Tensor, rois: torch.Tensor, roi_inds: torch.Tenso
                            f"{tuple(roi_inds.shape)}")
     ph, pw = (output_size, output_size) if isinstance(output_size, int) else tuple(output_size)
     x = _to_dev(input)
-    return _RoIPoolHeadFunction.apply(x.contiguous(), _to_dev(rois), _to_dev(roi_inds), int(ph), int(pw),
-                                      float(img_h), float(img_w), float(spatial_scale), bool(rois_sorted))
+    args = (x, _to_dev(rois), _to_dev(roi_inds), int(ph), int(pw), float(img_h), float(img_w),
+            float(spatial_scale), bool(rois_sorted))
+    if not (torch.is_grad_enabled() and x.requires_grad):  # inference: no autograd node
+        return _roi_pool_head_fwd(*args)
+    return _RoIPoolHeadFunction.apply(*args)
 
 
 def _boxes_to_rois(boxes: Union[torch.Tensor, List[torch.Tensor]]) -> torch.Tensor:
@@ -221,7 +232,7 @@ def propose(scores: torch.Tensor, deltas: torch.Tensor, *, img_w: float, img_h: 
                 or idx.dtype != torch.int32 or cnt.dtype != torch.int32):
             raise RuntimeError("propose: out buffers must be fp32 [N,post,4], int32 [N,post], int32 [N]")
     need = lib.frcnn_propose_workspace_size(p)
-    ws = workspace if workspace is not None else _lib.workspace(need, dev)
+    ws = workspace if workspace is not None else _lib.cached_workspace("propose", need, dev)
     if ws.numel() < need:
         raise RuntimeError(f"propose: workspace of {ws.numel()} B < {need} B")
     _lib.check(lib.frcnn_propose(p, _lib.ptr(scores), _lib.ptr(deltas), _lib.ptr(anchors),

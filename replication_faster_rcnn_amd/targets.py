@@ -43,7 +43,7 @@ def anchor_targets(boxes, labels, anchors, n_sample=256, pos_iou_thresh=0.7, neg
     lab = torch.empty((N, A), dtype=torch.int32, device=dev)
     am = torch.empty((N, A), dtype=torch.int32, device=dev) if internals else None
     mx = torch.empty((N, A), dtype=torch.float64, device=dev) if internals else None
-    ws = _lib.workspace(lib.frcnn_anchor_target_workspace_size(N, A, G), dev)
+    ws = _lib.cached_workspace("anchor_target", lib.frcnn_anchor_target_workspace_size(N, A, G), dev)
     own = rng is None
     if own:
         rng, st = rng_state_to_device(dev) if sample else (None, None)
@@ -81,7 +81,8 @@ def proposal_targets(rois, rcount, boxes, labels, n_sample=128, pos_ratio=0.5, p
     # utils/utils.py:272 subtracts / divides np.float32 arrays
     mean = np.asarray(reg_normalize_mean, np.float32).astype(np.float64)
     std = np.asarray(reg_normalize_std, np.float32).astype(np.float64)
-    ws = _lib.workspace(lib.frcnn_proposal_target_workspace_size(N, Rp, G, n_sample), dev)
+    ws = _lib.cached_workspace("proposal_target",
+                                lib.frcnn_proposal_target_workspace_size(N, Rp, G, n_sample), dev)
     own = rng is None
     if own:
         rng, st = rng_state_to_device(dev)

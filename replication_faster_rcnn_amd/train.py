@@ -73,7 +73,8 @@ class Trainer:
         sample_rois_ind = torch.arange(N, device=dev, dtype=torch.float32).repeat_interleave(S)
         reg_targets_classifier = s_reg.float()                                     # :89,103
         cls_labels_classifier = s_lab.float()                                      # :90,104
-        cls_output, reg_output = self.head(features, sample_rois, sample_rois_ind, img_h, img_w)
+        cls_output, reg_output = self.head(features, sample_rois, sample_rois_ind, img_h, img_w,
+                                           rois_sorted=True)  # grouped by construction
         # train.py:112-117: gather the regression of each sample's class
         reg_ind = cls_labels_classifier.detach().unsqueeze(-1).long() * 4
         reg_ind = torch.cat([reg_ind, reg_ind + 1, reg_ind + 2, reg_ind + 3], dim=-1)

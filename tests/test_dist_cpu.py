@@ -40,10 +40,10 @@ def _worker(rank, world, port, n_total, post, q):
     from oracle import ref_numpy as orc
     anchors = orc.generate_anchors(orc.generate_anchor_base(), 16, 20, 15)
     mine = [_proposals(img, anchors, post) for img in fdist.shard(n_total, rank, world)]
-    rois = torch.from_numpy(np.stack([m[0] for m in mine]))
-    idx = torch.from_numpy(np.stack([m[1] for m in mine]))
+    rois = torch.from_numpy(np.stack([m[0] for m in mine])) if mine else torch.zeros((0, post, 4))
+    idx = torch.from_numpy(np.stack([m[1] for m in mine])) if mine else torch.zeros((0, post), dtype=torch.int32)
     cnt = torch.tensor([m[2] for m in mine], dtype=torch.int32)
-    g = fdist.all_gather_detections(rois, idx, cnt)
+    g = fdist.all_gather_detections(rois, idx, cnt, n_total)
     if rank == 0:
         q.put([t.numpy() for t in g])
     dist.barrier()
@@ -56,7 +56,7 @@ def test_shard_covers_batch():
         assert got == list(range(n))
 
 
-@pytest.mark.parametrize("world,n_total", [(2, 4), (4, 8)])
+@pytest.mark.parametrize("world,n_total", [(2, 4), (4, 8), (4, 10), (4, 3)])
 def test_rank_gather_is_p_invariant(world, n_total):
     post = 50
     ctx = mp.get_context("spawn")
@@ -66,6 +66,7 @@ def test_rank_gather_is_p_invariant(world, n_total):
     for p in procs:
         p.start()
     rois, idx, cnt = q.get(timeout=120)
+    assert len(cnt) == n_total  # uneven (3/3/3/1) and empty (1/1/1/0) shards padded, then trimmed
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -13,19 +13,19 @@ import torch
 
 from oracle import ref_numpy as orc
 from replication_faster_rcnn_amd import anchors as A
-from replication_faster_rcnn_amd import ops, synth
+from replication_faster_rcnn_amd import _lib, ops, synth
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 RTOL = 1e-5
 
 
-@pytest.fixture(params=["fused", "lazy", "wide"])
-def path(request, monkeypatch):
+@pytest.fixture(params=["hybrid", "lazy", "wide"])
+def path(request):
     """The proposal paths: fused per-image with the chip-wide first-chunk mask
     (default), fused lazy per-block, chip-wide bitmask NMS."""
-    monkeypatch.setenv("FRCNN_PROPOSE_PATH", request.param)
-    return request.param
+    with _lib.kernel_path("propose", request.param):
+        yield request.param
 
 
 def sha(a):
@@ -244,13 +244,11 @@ def test_propose_edge_cases(case, path):
     assert np.array_equal(rois[0, :k].cpu().numpy(), orois)
 
 
-@pytest.mark.parametrize("variant", ["px8w16", "px8s", "px8", "pxf8", "pxf4", "wave8", "wave4", "tile"])
-def test_roi_pool_special_values(variant, monkeypatch):
-    """Signed zeros, -FLT_MAX, +-inf and NaN inside pooling windows: every
-    variant must reproduce the reference's strict-'>' first-max scan bit for bit."""
-    monkeypatch.setenv("FRCNN_ROIPOOL_VARIANT", variant)
-    r = np.random.default_rng(7)
-    N, C, H, W = 2, 16, 12, 14
+# forward paths: (kernel path, RoIs promised grouped by image)
+FWD_PATHS = [("dense", True), ("dense", False), ("generic", False)]
+
+
+def _special_x(r, N=2, C=16, H=12, W=14):
     x = r.standard_normal((N, C, H, W)).astype(np.float32)
     x[0, 0] = 0.0
     x[0, 0, ::2, ::3] = -0.0                       # +-0 ties: first zero's sign wins
@@ -261,34 +259,49 @@ def test_roi_pool_special_values(variant, monkeypatch):
     x[1, 5] = np.nan
     x[1, 6, :, 5] = 7.0                            # column plateau of equal maxima
     x[1, 7] = -0.0
+    x[1, 8:16] = np.round(x[1, 8:16])
+    x[1, 9] = np.maximum(x[1, 9], 0.0)             # ReLU: zero maxima, some -0
+    x[1, 9, 1::4, ::3] = -0.0
+    return x
+
+
+@pytest.mark.parametrize("fpath,sorted_", FWD_PATHS)
+def test_roi_pool_special_values(fpath, sorted_):
+    """Signed zeros, -FLT_MAX, +-inf and NaN inside pooling windows, RoIs partly /
+    fully outside the map: every path reproduces the reference's strict-'>'
+    first-max scan bit for bit (values compared as bits)."""
+    r = np.random.default_rng(7)
+    x = _special_x(r)
+    N = x.shape[0]
     rois = np.array([[b, x1, y1, x1 + w, y1 + h] for b in range(N) for (x1, y1, w, h) in
-                     [(0, 0, 13, 11), (1, 2, 5, 3), (3, 3, 0, 0), (2, 1, 9, 9), (-3, -2, 20, 20)]],
-                    np.float32)
-    out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7)
+                     [(0, 0, 13, 11), (1, 2, 5, 3), (3, 3, 0, 0), (2, 1, 9, 9), (-3, -2, 20, 20),
+                      (10, 8, 30, 30), (-20, -20, 5, 5), (4, 1, 1.4, 7)]], np.float32)
+    if not sorted_:
+        rois = rois[r.permutation(len(rois))]
+    with _lib.kernel_path("roi_pool_fwd", fpath):
+        out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7,
+                                           rois_sorted=sorted_)
     oo, oa = orc.roi_pool_forward(x, rois, 7)
     assert np.array_equal(am.cpu().numpy(), oa)
     assert np.array_equal(out.cpu().numpy().view(np.uint32), oo.view(np.uint32))
 
 
-@pytest.mark.parametrize("variant", ["sorted", "px8sorted", "px8w16", "px8s", "px8", "pxf8", "pxf4",
-                                     "wave8", "wave4", "tile"])
-def test_roi_pool_variants_random(variant, monkeypatch):
-    """Every forward variant, cfg2-like random RoIs, bit-exact vs the oracle
-    ("sorted" = the default single-launch path for RoIs grouped by image)."""
-    if variant == "sorted":
-        monkeypatch.delenv("FRCNN_ROIPOOL_VARIANT", raising=False)
-    else:
-        monkeypatch.setenv("FRCNN_ROIPOOL_VARIANT", variant)
+@pytest.mark.parametrize("fpath,sorted_", FWD_PATHS)
+def test_roi_pool_paths_random(fpath, sorted_):
+    """Every forward path, cfg2-like random RoIs with plenty of ties, bit-exact vs the oracle."""
     r = np.random.default_rng(11)
     N, C, H, W, R = 3, 32, 38, 63, 600
     x = r.standard_normal((N, C, H, W), dtype=np.float32)
     x[:, :, 10:20, 10:30] = np.round(x[:, :, 10:20, 10:30])  # plenty of ties
     b = np.sort(r.integers(0, N, R)).astype(np.float32)
+    if not sorted_:
+        r.shuffle(b)
     xy = r.uniform(-3, 60, (R, 2)).astype(np.float32)
     wh = r.uniform(0, 40, (R, 2)).astype(np.float32)
     rois = np.concatenate([b[:, None], xy, xy + wh], 1).astype(np.float32)
-    out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7,
-                                       rois_sorted=variant in ("sorted", "px8sorted"))
+    with _lib.kernel_path("roi_pool_fwd", fpath):
+        out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7,
+                                           rois_sorted=sorted_)
     oo, oa = orc.roi_pool_forward(x, rois, 7)
     assert np.array_equal(am.cpu().numpy(), oa)
     assert np.array_equal(out.cpu().numpy(), oo)
@@ -300,42 +313,40 @@ def _rand_rois(r, b, H, W, lo=-3, span=40):
     return np.concatenate([np.asarray(b, np.float32)[:, None], xy, xy + wh], 1).astype(np.float32)
 
 
-@pytest.mark.parametrize("variant", ["bal2", "bal", "px8q@1", "px8q@3", "px8q@64", "px8r@1", "px8r@2", "px8r@5", "px16@1", "px16@3"])
-@pytest.mark.parametrize("case", ["many_images", "invalid_ends", "unsorted_promised_sorted",
-                                  "single_roi", "gaps", "one_image_tiny_rois", "uniform_sizes",
-                                  "ph5", "cfg4_shape"])
-def test_roi_pool_balanced_path(case, variant, monkeypatch):
-    """The cost-balanced single-launch forward (default for RoIs grouped by
-    image): segment boundaries, run lists (and their overflow / block-search
-    fallback), out-of-range batch indices, and any RoI order bit-exact.
-    px8q / px8r (strided per-image shares, `@k` = shares per image) need the
-    promised grouping, so it skips the unsorted case."""
-    variant, _, split = variant.partition("@")
-    if variant.startswith(("px8q", "px8r", "px16")) and case == "unsorted_promised_sorted":
-        pytest.skip("px8q requires RoIs grouped by image")
-    monkeypatch.setenv("FRCNN_ROIPOOL_VARIANT", variant)
-    if split:
-        monkeypatch.setenv("FRCNN_ROIPOOL_SPLIT", split)
+@pytest.mark.parametrize("split", ["auto", "1", "3", "64"])
+@pytest.mark.parametrize("case", ["many_images", "invalid_ends", "unsorted", "single_roi", "gaps",
+                                  "one_image_tiny_rois", "uniform_sizes", "ph5", "ph8x8", "ph3x9",
+                                  "cfg4_shape", "c8", "c4"])
+def test_roi_pool_dense_cases(case, split):
+    """The dense image-tile forward: cost-balanced shares (`split` per image),
+    geometry chunks, window-class ordering, bins packed across RoIs for any
+    PH x PW <= 64, out-of-range batch indices, 16 / 8 / 4-channel tiles, and any
+    RoI order (per-image lists) -- bit-exact vs the oracle."""
     r = np.random.default_rng(sum(map(ord, case)))
-    ph = 5 if case == "ph5" else 7
+    ph, pw = {"ph5": (5, 5), "ph8x8": (8, 8), "ph3x9": (3, 9)}.get(case, (7, 7))
     N, C, H, W = 4, 16, 20, 27
     span = 40
-    if case == "many_images":  # > 32 runs per segment and > 2 run starts per thread chunk
+    sorted_ = case != "unsorted"
+    if case == "many_images":  # more images than one geometry chunk
         N, C, H, W, span = 20000, 8, 4, 5, 6
         b = np.sort(r.integers(0, N, 40000))
     elif case == "invalid_ends":
         b = np.concatenate([[-1, -1], np.sort(r.integers(0, N, 200)), [N, N, N + 3]])
-    elif case == "unsorted_promised_sorted":
-        b = r.integers(0, N, 500)
+    elif case == "unsorted":
+        b = np.concatenate([r.integers(0, N, 500), [-1, N + 2]])
+        r.shuffle(b)
     elif case == "single_roi":
         b = np.array([2])
     elif case == "gaps":  # images 1 and 2 have no RoIs
         b = np.sort(np.concatenate([np.zeros(60, int), np.full(90, 3)]))
-    elif case == "cfg4_shape":  # 50x84 tile: one workgroup per CU
+    elif case == "cfg4_shape":  # 50x84 tile: 8-channel planes, one workgroup per CU
         N, C, H, W = 1, 16, 50, 84
         b = np.zeros(500, int)
-    elif case == "one_image_tiny_rois":
-        N, b, span = 1, np.zeros(3000, int), 2
+    elif case == "one_image_tiny_rois":  # > one geometry chunk per workgroup
+        N, b, span = 1, np.zeros(6000, int), 2
+    elif case in ("c8", "c4"):
+        C = 8 if case == "c8" else 12
+        b = np.sort(r.integers(0, N, 300))
     else:
         b = np.sort(r.integers(0, N, 700))
     x = r.standard_normal((N, C, H, W), dtype=np.float32)
@@ -343,82 +354,78 @@ def test_roi_pool_balanced_path(case, variant, monkeypatch):
     rois = _rand_rois(r, b, H, W, span=span)
     if case == "uniform_sizes":
         rois[:, 3:] = rois[:, 1:3] + 6.0
-    out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), ph,
-                                       rois_sorted=True)
-    oo, oa = orc.roi_pool_forward(x, rois, ph)
+    with _lib.kernel_path("roi_pool_split", split):
+        out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV),
+                                           (ph, pw), rois_sorted=sorted_)
+    oo, oa = orc.roi_pool_forward(x, rois, (ph, pw))
     valid = (b >= 0) & (b < N)
     assert np.array_equal(am.cpu().numpy()[valid], oa[valid])
     assert np.array_equal(out.cpu().numpy()[valid].view(np.uint32), oo[valid].view(np.uint32))
     assert (out.cpu().numpy()[~valid] == 0).all() and (am.cpu().numpy()[~valid] == -1).all()
 
 
-@pytest.mark.parametrize("variant", ["px16", "px8r", "px8q", "bal2", "bal2ns", "bal", "px8sorted"])
-def test_roi_pool_sorted_variants_cfg2(variant, monkeypatch):
-    """The two single-launch forwards for image-grouped RoIs at the bench shape
-    (8 x 256 x 38 x 63, 300 proposals per image) agree bit for bit with the
-    oracle on a sample of images."""
-    monkeypatch.setenv("FRCNN_ROIPOOL_VARIANT", variant)
+@pytest.mark.parametrize("sorted_", [True, False])
+def test_roi_pool_cfg2_shape(sorted_):
+    """The bench shape (8 x 256 x 38 x 63, 300 RoIs per image): dense forward
+    bit for bit vs the oracle on a sample of RoIs from every image."""
     r = np.random.default_rng(5)
     N, C, H, W, per = 8, 256, 38, 63, 300
     x = r.standard_normal((N, C, H, W), dtype=np.float32)
     b = np.repeat(np.arange(N), per)
     rois = _rand_rois(r, b, H, W, span=45)
+    perm = np.arange(len(b)) if sorted_ else r.permutation(len(b))
+    rois = rois[perm]
     out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7,
-                                       rois_sorted=True)
-    pick = np.concatenate([np.arange(0, 40), np.arange(1190, 1230), np.arange(2360, 2400)])
+                                       rois_sorted=sorted_)
+    pick = np.concatenate([np.arange(i * per, i * per + 25) for i in range(N)] + [np.arange(2390, 2400)])
     oo, oa = orc.roi_pool_forward(x, rois[pick], 7)
     assert np.array_equal(am.cpu().numpy()[pick], oa)
     assert np.array_equal(out.cpu().numpy()[pick], oo)
 
 
-@pytest.mark.parametrize("variant", ["px16", "px8r", "px8q", "bal2", "bal2ns", "bal", "px8sorted"])
-def test_roi_pool_sorted_special_values(variant, monkeypatch):
-    """The image-grouped forwards on signed zeros, -FLT_MAX, +-inf and NaN
-    windows, RoIs partly / fully outside the map (bal2: clamped revisits and
-    the -inf pad pixel) -- bit-exact vs the oracle."""
-    monkeypatch.setenv("FRCNN_ROIPOOL_VARIANT", variant)
-    r = np.random.default_rng(7)
-    N, C, H, W = 2, 16, 12, 14
-    x = r.standard_normal((N, C, H, W)).astype(np.float32)
-    x[0, 0] = 0.0
-    x[0, 0, ::2, ::3] = -0.0
-    x[0, 1] = -np.float32(3.4028235e38)
-    x[0, 2] = -np.inf
-    x[0, 3, ::2] = np.nan
-    x[0, 4, 3:6, 3:6] = np.inf
-    x[1, 5] = np.nan
-    x[1, 6, :, 5] = 7.0
-    x[1, 7] = -0.0
-    x[1, 8:16] = np.round(x[1, 8:16])
-    rois = np.array([[b, x1, y1, x1 + w, y1 + h] for b in range(N) for (x1, y1, w, h) in
-                     [(0, 0, 13, 11), (1, 2, 5, 3), (3, 3, 0, 0), (2, 1, 9, 9), (-3, -2, 20, 20),
-                      (10, 8, 30, 30), (-20, -20, 5, 5)]], np.float32)
-    out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7,
-                                       rois_sorted=True)
-    oo, oa = orc.roi_pool_forward(x, rois, 7)
+def test_roi_pool_cfg4_full_shape():
+    """BASELINE configs[3] in full: 1 x 512 x 50 x 84 features, 2000 proposals of
+    an 800x1333 image through the head's transform + RoIPool (one launch), every
+    output and argmax bit-exact vs the oracle; gradient bit-exact too."""
+    c = synth.CONFIGS["cfg4"]
+    r = np.random.default_rng(44)
+    H, W, C, R = c["feat_h"], c["feat_w"], c["C"], c["post_nms"]
+    x = synth.features(C, H, W, 0, 0)[None]
+    y1 = r.uniform(-20, c["img_h"], R).astype(np.float32)
+    x1 = r.uniform(-20, c["img_w"], R).astype(np.float32)
+    rois = np.stack([y1, x1, y1 + r.uniform(8, 520, R).astype(np.float32),
+                     x1 + r.uniform(8, 700, R).astype(np.float32)], 1).astype(np.float32)
+    inds = np.zeros(R, np.float32)
+    xt = torch.from_numpy(x).to(DEV).requires_grad_(True)
+    out, am, boxes = ops.roi_pool_head(xt, torch.from_numpy(rois).to(DEV), torch.from_numpy(inds).to(DEV),
+                                       7, c["img_h"], c["img_w"], rois_sorted=True)
+    oboxes = orc.roi_transform(rois, inds, c["img_h"], c["img_w"], H, W)
+    assert np.array_equal(boxes.cpu().numpy(), oboxes)
+    oo, oa = orc.roi_pool_forward(x, oboxes, 7)
     assert np.array_equal(am.cpu().numpy(), oa)
-    assert np.array_equal(out.cpu().numpy().view(np.uint32), oo.view(np.uint32))
+    assert np.array_equal(out.detach().cpu().numpy(), oo)
+    g = torch.from_numpy(r.standard_normal(out.shape, dtype=np.float32)).to(DEV)
+    (out * g).sum().backward()
+    og = orc.roi_pool_backward(g.cpu().numpy(), oboxes, oa, x.shape)
+    assert np.array_equal(xt.grad.cpu().numpy(), og)
 
 
 @pytest.mark.parametrize("case", ["grouped", "grouped_split3", "grouped_cg8", "ungrouped", "out_of_range",
                                   "c_not8", "many_per_image"])
-def test_roi_pool_head_fused(case, monkeypatch):
+def test_roi_pool_head_fused(case):
     """ops.roi_pool_head = nets/heads.py:42-48 (transform + pack + roi_pool) in
     one call: boxes, out and argmax bit-exact vs the oracle's roi_transform +
     roi_pool, and its gradient identical to roi_pool's on the same boxes."""
-    monkeypatch.delenv("FRCNN_ROIPOOL_VARIANT", raising=False)
-    if case == "grouped_split3":
-        monkeypatch.setenv("FRCNN_ROIPOOL_SPLIT", "3")
-    if case == "grouped_cg8":
-        monkeypatch.setenv("FRCNN_ROIPOOL_VARIANT", "px8q")
+    split = {"grouped_split3": "3", "many_per_image": "1"}.get(case, "auto")
     r = np.random.default_rng(sum(map(ord, case)))
     N, C, H, W, img_h, img_w = 3, 16, 38, 63, 600.0, 1000.0
     if case == "c_not8":
         C = 12
+    if case == "grouped_cg8":
+        C = 24
     R = 257
     if case == "many_per_image":  # > geo_cap RoIs per workgroup: several geometry chunks
-        N, C, R = 1, 16, 3000
-        monkeypatch.setenv("FRCNN_ROIPOOL_SPLIT", "1")
+        N, C, R = 1, 16, 9000
     inds = np.sort(r.integers(0, N, R)).astype(np.float32)
     if case == "ungrouped":
         r.shuffle(inds)
@@ -433,8 +440,9 @@ def test_roi_pool_head_fused(case, monkeypatch):
     x = r.standard_normal((N, C, H, W), dtype=np.float32)
     x[:, :, 5:15, 5:25] = np.round(x[:, :, 5:15, 5:25])  # ties
     xt = torch.from_numpy(x).to(DEV).requires_grad_(True)
-    out, am, boxes = ops.roi_pool_head(xt, torch.from_numpy(rois).to(DEV), torch.from_numpy(inds).to(DEV),
-                                       7, img_h, img_w, rois_sorted=case != "ungrouped")
+    with _lib.kernel_path("roi_pool_split", split):
+        out, am, boxes = ops.roi_pool_head(xt, torch.from_numpy(rois).to(DEV), torch.from_numpy(inds).to(DEV),
+                                           7, img_h, img_w, rois_sorted=case != "ungrouped")
     oboxes = orc.roi_transform(rois, inds, img_h, img_w, H, W)
     assert np.array_equal(boxes.cpu().numpy().view(np.uint32), oboxes.view(np.uint32))
     oo, oa = orc.roi_pool_forward(x, oboxes, 7)
@@ -448,7 +456,7 @@ def test_roi_pool_head_fused(case, monkeypatch):
     assert np.array_equal(xt.grad.cpu().numpy(), og)
 
 
-def test_roi_pool_bwd_ring_equals_plain(monkeypatch):
+def test_roi_pool_bwd_ring_equals_plain():
     """The latency-hidden backward (8-RoI load ring) and the plain plane-owner
     kernel give identical bits, incl. duplicated RoIs (same argmax pixels across
     RoIs and bins), images with 0 / fewer than 8 / 8k+r RoIs."""
@@ -468,8 +476,8 @@ def test_roi_pool_bwd_ring_equals_plain(monkeypatch):
     out, am = ops.roi_pool_with_argmax(x, rois, 7)
     g = torch.randn(out.shape, device=DEV)
     a = _roi_pool_bwd(g, rois, am, x.shape, 1.0)
-    monkeypatch.setenv("FRCNN_BWD_VARIANT", "plain")
-    b = _roi_pool_bwd(g, rois, am, x.shape, 1.0)
+    with _lib.kernel_path("roi_pool_bwd", "plain"):
+        b = _roi_pool_bwd(g, rois, am, x.shape, 1.0)
     assert torch.equal(a, b)
     ref = orc.roi_pool_backward(g.cpu().numpy(), rois.cpu().numpy(), am.cpu().numpy(), x.shape)
     assert np.array_equal(a.cpu().numpy(), ref)

@@ -1,8 +1,8 @@
-"""A/B timing of the proposal paths (FRCNN_PROPOSE_PATH = fused | lazy | wide)
+"""A/B timing of the proposal paths (frcnn_set_path("propose", hybrid | lazy | wide))
 on the bench inputs, interleaved rounds; every path's output is checked
 bit-equal to the first path's.
 
-    python tools/ab_propose.py [--config cfg2] [--paths fused,lazy,wide]
+    python tools/ab_propose.py [--config cfg2] [--paths hybrid,lazy,wide]
 """
 import argparse
 import json
@@ -14,19 +14,20 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import make_inputs  # noqa: E402
-from replication_faster_rcnn_amd import anchors as A, ops, synth  # noqa: E402
+from replication_faster_rcnn_amd import _lib, ops, synth  # noqa: E402
+from replication_faster_rcnn_amd import anchors as A  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg2")
-    ap.add_argument("--paths", default="fused,lazy,wide")
+    ap.add_argument("--paths", default="hybrid,lazy,wide")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     c = synth.CONFIGS[a.config]
-    c, sc, de, x = make_inputs(a.config, c["batch"], 0, dev)
+    c, sc, de, x = make_inputs(a.config, range(c["batch"]), dev)
     base = A.generate_anchor_base_device(anchor_scales=c["scales"])
 
     def run():
@@ -39,7 +40,7 @@ def main():
     ref = None
     for rnd in range(a.rounds):
         for p in paths:
-            os.environ["FRCNN_PROPOSE_PATH"] = p
+            _lib.set_path("propose", p)
             out = run()
             if ref is None:
                 ref = [t.clone() for t in out]

@@ -1,11 +1,13 @@
-"""A/B timing of RoIPool forward variants on one device, interleaved rounds.
+"""A/B timing of the RoIPool forward paths on one device, interleaved rounds.
 
-    python tools/ab_roi_pool.py [--config cfg2] [--variants wave4,wave8,tile,px8q@4]
+    python tools/ab_roi_pool.py [--config cfg2] [--variants dense,dense@3,unsorted,generic]
 
-`name@k` runs variant `name` with FRCNN_ROIPOOL_SPLIT=k (RoI shares per image).
+`name@k` runs `name` with frcnn_set_path("roi_pool_split", k) (RoI shares per
+image).  Names: dense (RoIs promised grouped by image, one launch), unsorted
+(per-image lists first), generic (one workgroup per RoI).
 
-Inputs are the bench's: cfg features + the proposals of the batch.  Every
-variant's output is checked bit-equal to the first variant's.
+Inputs are the bench's: the config's features + the proposals of the batch.
+Every variant's output is checked bit-equal to the first variant's.
 """
 import argparse
 import json
@@ -17,19 +19,20 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import make_inputs  # noqa: E402
-from replication_faster_rcnn_amd import anchors as A, ops, synth  # noqa: E402
+from replication_faster_rcnn_amd import _lib, ops, synth  # noqa: E402
+from replication_faster_rcnn_amd import anchors as A  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg2")
-    ap.add_argument("--variants", default="sorted,px8w16,px8")
+    ap.add_argument("--variants", default="dense,unsorted")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     c = synth.CONFIGS[a.config]
-    c, sc, de, x = make_inputs(a.config, c["batch"], 0, dev)
+    c, sc, de, x = make_inputs(a.config, range(c["batch"]), dev)
     N = sc.size(0)
     base = A.generate_anchor_base_device(anchor_scales=c["scales"])
     rois, idx, cnt = ops.propose(sc, de, img_w=c["img_w"], img_h=c["img_h"], pre_nms=c["pre_nms"],
@@ -46,19 +49,13 @@ def main():
     for rnd in range(a.rounds):
         for vs in variants:
             v, _, sp = vs.partition("@")
-            if sp:
-                os.environ["FRCNN_ROIPOOL_SPLIT"] = sp
-            else:
-                os.environ.pop("FRCNN_ROIPOOL_SPLIT", None)
-            srt = v in ("px16p", "px16", "px16S", "px8r", "px8rS", "px8q", "px8qn", "px8qS", "px8qC", "sorted", "bal", "balcnt", "px8sorted", "balnc", "balns", "bal2", "bal2ns", "bal2c", "bal2b")  # single-launch paths (RoIs grouped by image)
-            if v == "sorted":
-                os.environ.pop("FRCNN_ROIPOOL_VARIANT", None)
-            else:
-                os.environ["FRCNN_ROIPOOL_VARIANT"] = v
+            _lib.set_path("roi_pool_split", sp or "auto")
+            _lib.set_path("roi_pool_fwd", "generic" if v == "generic" else "auto")
+            srt = v == "dense"
             out, am = ops._roi_pool_fwd(x, boxes, 7, 7, 1.0, srt)
             if ref is None:
                 ref = (out.clone(), am.clone())
-            elif rnd == 0 and v not in ("px16S", "px8rS", "px8qS", "px8qC", "balnc", "balns", "bal2c", "bal2b"):
+            elif rnd == 0:
                 assert torch.equal(out, ref[0]) and torch.equal(am, ref[1]), f"variant {vs} differs"
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -67,6 +64,8 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             times[vs].append(e0.elapsed_time(e1) / a.iters * 1e3)
+    _lib.set_path("roi_pool_split", "auto")
+    _lib.set_path("roi_pool_fwd", "auto")
     res = {v: {"us_median": float(np.median(t)), "us_min": float(np.min(t)),
                "GBps": alg / (np.median(t) * 1e-6) / 1e9} for v, t in times.items()}
     print(json.dumps({"config": a.config, "R": R, "alg_bytes": alg, "variants": res}, indent=1))

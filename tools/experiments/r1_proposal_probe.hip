@@ -496,6 +496,15 @@ __device__ uint64_t select_rank(const uint32_t (&sk)[KPT], int A, unsigned r, un
 //   MODE 2 (one workgroup per image): greedy sweep of the chunk from those
 //          bits (chunk_sweep), then the lazy path from the second chunk on --
 //          only if the first chunk kept fewer than post_nms boxes.
+// tools-only timeline probe (tools/prop_timeline.py): when g_prop_probe is set,
+// thread 0 of image n < 64 stamps s_memrealtime (100 MHz) at phase ends.
+__device__ int g_prop_probe;
+__device__ unsigned long long g_prop_dbg[64 * 16];
+#define FRCNN_PROBE(k)                                                                         \
+    do {                                                                                       \
+        if (probe && threadIdx.x == 0 && blockIdx.x < 64)                                      \
+            g_prop_dbg[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime();              \
+    } while (0)
 
 struct HybWs {
     float4* cbox;    // [N][kChunk] first-chunk boxes, score order
@@ -620,6 +629,8 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
 
     const int n = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const bool probe = g_prop_probe != 0;
+    FRCNN_PROBE(MODE == 2 ? 8 : 0);
     const uint64_t* keys = keys_all + static_cast<size_t>(n) * A;
     const float4* boxes = boxes_all + static_cast<size_t>(n) * A;
     float4* orois = out_rois + static_cast<size_t>(n) * post;
@@ -641,6 +652,7 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
             ckey[i] = hw.ckey[static_cast<size_t>(n) * kChunk + i];
         }
         __syncthreads();
+        FRCNN_PROBE(9);
         kcount = chunk_sweep(hw.colT + static_cast<size_t>(n) * kChunk * kChunkBlocks, cc, post, cbox,
                              carea, ckey, kbox, karea, orois, oidx, sh);
         r_done = cc;
@@ -649,6 +661,7 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
             have_prev = true;
         }
         if (tid == 0) sh.kcount = kcount;
+        FRCNN_PROBE(10);
     }
     if (MODE != 2 || (kcount < post && r_done < P)) {  // the keys are needed (uniform)
         unsigned nv = 0;
@@ -669,12 +682,14 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
             P = static_cast<int>(M < static_cast<unsigned>(pre) ? M : static_cast<unsigned>(pre));
         }
         __syncthreads();
+        FRCNN_PROBE(1);
     }
     while (r_done < P && kcount < post) {
         const int r_end = min(r_done + kChunk, P);
         const uint64_t T = select_rank<KPT>(sk, A, static_cast<unsigned>(r_end), hist, sh);
         if (tid == 0) sh.ccount = 0;
         __syncthreads();
+        if (r_done == 0) FRCNN_PROBE(2);
 #pragma unroll
         for (int k = 0; k < KPT; ++k) {
             const int a = tid + k * 1024;
@@ -684,6 +699,7 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
             }
         }
         __syncthreads();
+        if (r_done == 0) FRCNN_PROBE(3);
         const int cc = r_end - r_done;  // == sh.ccount (keys are unique)
         // ---- sort of the chunk, ascending: every wave bitonic-sorts its 64 keys
         // with shuffles; a key's final position is its rank = the number of keys
@@ -719,6 +735,7 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
         if (key != kInvalidKey) ckey[rank] = key;
         __syncthreads();
         key = ckey[tid];
+        if (r_done == 0) FRCNN_PROBE(4);
         ckey[tid] = key;
         if (tid < cc) {
             const float4 b = boxes[static_cast<uint32_t>(key)];
@@ -726,6 +743,7 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
             carea[tid] = box_area(b);
         }
         __syncthreads();
+        if (r_done == 0) FRCNN_PROBE(5);
         if (MODE == 1) {  // hand the sorted first chunk to chunk_colmask_kernel
             if (tid < cc) {
                 hw.cbox[static_cast<size_t>(n) * kChunk + tid] = cbox[tid];
@@ -735,6 +753,7 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
                 hw.cc[n] = cc;
                 hw.P[n] = P;
             }
+            FRCNN_PROBE(6);
             return;
         }
         // ---- lazy NMS over 64-candidate blocks
@@ -813,6 +832,7 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
         oidx[s] = -1;
     }
     if (tid == 0) out_count[n] = kcount;
+    FRCNN_PROBE(MODE == 2 ? 11 : 7);
 }
 
 static size_t fused_lds_bytes(int post) {
@@ -852,10 +872,10 @@ static int launch_fused(const uint64_t* keys, const float4* boxes, int N, int A,
 // does O(rows x kept) IoU work; the wide path spreads an O(pre^2/2) bitmask
 // over the whole chip.  Few images with a large post_nms -> wide.
 static bool use_fused(int N, int A, int post) {
+    const char* force = getenv("FRCNN_PROPOSE_PATH");  // test / bench override
     if (A > kFusedMaxA || post > 4096) return false;
-    const int forced = path_cfg().propose;  // frcnn_set_path("propose", ...)
-    if (forced == kPathHybrid || forced == kPathLazy) return true;
-    if (forced == kPathWide) return false;
+    if (force && (force[0] == 'f' || force[0] == 'l')) return true;  // fused hybrid / fused lazy
+    if (force && force[0] == 'w') return false;
     return N >= 4 || post <= 1000;
 }
 
@@ -971,9 +991,10 @@ extern "C" int frcnn_propose(const frcnn_propose_params* p, const float* scores,
                        p->feat_stride, p->img_h, p->img_w, p->min_size, w.boxes, w.keys);
     FRCNN_LAUNCH_CHECK("decode_filter_kernel");
     if (use_fused(p->N, p->A, p->post_nms)) {
+        const char* force = getenv("FRCNN_PROPOSE_PATH");  // 'l': the lazy fused path (A/B, tests)
         return launch_fused(w.keys, w.boxes, p->N, p->A, pre, p->post_nms, make_thr(p->iou_threshold),
                             reinterpret_cast<float4*>(out_rois), out_idx, out_count, w.hyb,
-                            path_cfg().propose == kPathLazy, st);
+                            force && force[0] == 'l', st);
     }
     return sort_and_suppress(w, w.boxes, p->N, p->A, pre, p->post_nms, p->iou_threshold, 0,
                              reinterpret_cast<float4*>(out_rois), out_idx, nullptr, out_count, st);
@@ -1006,3 +1027,11 @@ extern "C" int frcnn_nms(const float* boxes, const float* scores, int64_t n, dou
                              1, nullptr, nullptr, keep, count, st);
 }
 
+// tools-only (not part of the C-ABI): switch the proposal timeline probe and read it
+extern "C" int frcnn_dbg_prop_probe(int on) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_prop_probe), &on, sizeof(int)) == hipSuccess ? 0 : -2;
+}
+extern "C" int frcnn_dbg_prop_stamps(unsigned long long* host, int n) {
+    if (n > 64 * 16) n = 64 * 16;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_prop_dbg), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -2;
+}
