@@ -154,27 +154,60 @@ def _host_info():
     return model, isa
 
 
+def _cgroup_cpus():
+    """CPUs this process may actually use per the cgroup CPU quota (v2 cpu.max
+    or v1 cfs_quota/period), None when unlimited / unreadable.  The GPU box
+    shows the whole machine in the affinity mask (256 CPUs) but grants a share
+    of it; torch on 256 threads over a 16-CPU share spins ~25x slower."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, int(-(-int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if q > 0:
+            return max(1, -(-q // p))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_threads():
+    """(threads used, affinity count, cgroup quota, OMP_NUM_THREADS)."""
+    aff = len(os.sched_getaffinity(0))
+    cg = _cgroup_cpus()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    omp = int(omp) if omp and omp.isdigit() and int(omp) > 0 else None
+    use = min(x for x in (aff, cg, omp) if x)
+    return use, aff, cg, omp
+
+
 def cpu_baseline(cfg, seconds, min_images, train=False):
     """The reference's CPU path per image (nets/rpn.py:58-77 in torch CPU ops,
     nets/heads.py:42-48; for cfg5 also the numpy target creators of
-    utils/utils.py:122-276 and the RoIPool backward), torch given every core of
-    this process's affinity; torchvision's nms / roi_pool are the oracle's C
-    restatement of their (single-threaded) CPU kernels.  >= 3 warm-up images,
-    then the median over >= `min_images` images (more while `seconds` last)."""
+    utils/utils.py:122-276 and the RoIPool backward), torch given every CPU
+    this process may use (affinity, capped by the cgroup quota and
+    OMP_NUM_THREADS -- the GPU box's affinity mask lists the whole machine);
+    torchvision's nms / roi_pool are the oracle's C restatement of their
+    (single-threaded) CPU kernels.  The thread count is the faster of that and
+    1 thread on 3 probe images (small torch ops can lose to threading).
+    >= 3 warm-up images, then the median over >= `min_images` images (more
+    while `seconds` last)."""
     from oracle import ref_numpy as orc
     from oracle import ref_torch as ort
     from replication_faster_rcnn_amd import synth
-    cores = len(os.sched_getaffinity(0))
-    torch.set_num_threads(cores)
+    cores, aff, cg, omp = cpu_threads()
     c = synth.CONFIGS[cfg]
     base = orc.generate_anchor_base(anchor_scales=c["scales"])
     anchors = orc.generate_anchors(base, 16, c["feat_w"], c["feat_h"])
     A = len(anchors)
     g = np.random.default_rng(1).standard_normal((128, c["C"], 7, 7), dtype=np.float32)
     np.random.seed(0)
-    times, t_all, i = [], time.perf_counter(), 0
-    warm = 3
-    while True:
+
+    def one(i):
         sc = torch.from_numpy(synth.rpn_scores(A, 0, i))
         de = torch.from_numpy(synth.rpn_deltas(A, 0, i))
         x = torch.from_numpy(synth.features(c["C"], c["feat_h"], c["feat_w"], 0, i)[None])
@@ -190,12 +223,24 @@ def cpu_baseline(cfg, seconds, min_images, train=False):
         out, am, boxes = ort.head_roi_pool(x, roi, torch.zeros(len(roi)), c["img_h"], c["img_w"])
         if train:
             orc.roi_pool_backward(g[:len(roi)], boxes.numpy(), am.numpy(), tuple(x.shape))
-        te = time.perf_counter()
+        return time.perf_counter() - ts
+
+    probe = {}
+    for th in sorted({cores, 1}, reverse=True):  # 1 warm-up + 2 timed images each
+        torch.set_num_threads(th)
+        probe[th] = min(one(k) for k in range(3))
+    threads = min(probe, key=probe.get)
+    torch.set_num_threads(threads)
+    times, t_all, i = [], time.perf_counter(), 3
+    warm = 3
+    while True:
+        dt = one(i)
         i += 1
         if warm:
             warm -= 1
             continue
-        times.append(te - ts)
+        times.append(dt)
+        te = time.perf_counter()
         if len(times) >= min_images and te - t_all >= seconds:
             break
         if len(times) >= 10 * min_images and te - t_all >= 3:
@@ -204,12 +249,14 @@ def cpu_baseline(cfg, seconds, min_images, train=False):
     model, isa = _host_info()
     what = "training step (proposals, anchor + proposal targets, RoIPool fwd+bwd)" if train else \
         "proposal layer + head RoIPool"
-    return {"value": 1.0 / med, "unit": "images/sec", "cores": cores, "kind": "port",
+    return {"value": 1.0 / med, "unit": "images/sec", "cores": threads, "kind": "port",
             "sample": f"{cfg} {what}, one image at a time like nets/rpn.py:131: median of "
                       f"{len(times)} images after 3 warm-ups ({sum(times):.1f} s timed); torch CPU ops "
-                      f"of the reference on {cores} threads, torchvision nms/roi_pool as the oracle's "
+                      f"of the reference on {threads} threads, torchvision nms/roi_pool as the oracle's "
                       f"single-threaded C restatement",
             "cpu_model": model, "cpu_isa": isa, "torch_threads": torch.get_num_threads(),
+            "affinity_cpus": aff, "cgroup_cpus": cg, "omp_num_threads": omp,
+            "probe_ms_per_image": {str(k): v * 1e3 for k, v in probe.items()},
             "median_ms_per_image": med * 1e3}
 
 

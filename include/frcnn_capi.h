@@ -40,10 +40,12 @@ int frcnn_device_cu_count(int* out);
 
 /* Kernel-path selection, process-global (tests and A/B tools; the default
  * "auto" is what every caller should use).  op / path:
- *   "roi_pool_fwd"   : "auto" | "dense" (image tile in LDS) | "generic" (one workgroup per RoI)
+ *   "roi_pool_fwd"   : "auto" | "sorted" (image tile in LDS, bins sorted by window shape)
+ *                      | "dense" (image tile, a RoI's bins per wave) | "generic" (one workgroup per RoI)
  *   "roi_pool_bwd"   : "auto" | "ring" (latency-hidden plane owner) | "plain"
  *   "propose"        : "auto" | "hybrid" | "lazy" (fused per image) | "wide" (chip-wide bitmask)
  *   "roi_pool_split" : "auto" | "1".."64" (RoI shares per image and channel group)
+ *   "roi_pool_cg"    : "auto" | "4" | "8" | "16" (channels per RoIPool forward workgroup)
  * All paths give bit-identical results.  Not thread-safe against calls in
  * flight on other threads; set it before launching. */
 int frcnn_set_path(const char* op, const char* path);

@@ -17,6 +17,8 @@ void set_error(const char* fmt, ...);
 // Read once per call as plain ints: no getenv on the launch path.
 constexpr int kPathAuto = 0;
 constexpr int kPathGeneric = 1;  // roi_pool_fwd: one workgroup per RoI
+constexpr int kPathDense = 2;    // roi_pool_fwd: image tile, RoI bins packed per wave
+constexpr int kPathSorted = 3;   // roi_pool_fwd: image tile, bins sorted by window shape
 constexpr int kPathPlain = 1;    // roi_pool_bwd: the unpipelined plane-owner kernel
 constexpr int kPathHybrid = 1;   // propose: fused per image + chip-wide first-chunk mask
 constexpr int kPathLazy = 2;     // propose: fused per image, lazy NMS from the first chunk on
@@ -26,6 +28,8 @@ struct PathCfg {
     int roi_bwd = kPathAuto;
     int propose = kPathAuto;
     int roi_split = 0;  // RoI shares per (image, channel group); 0 = auto
+    int roi_cg = 0;     // channels per RoIPool workgroup (4 / 8 / 16); 0 = auto
+    int roi_probe = 0;  // TEMPORARY timing probe: 1 = sorted forward without its output stores
 };
 const PathCfg& path_cfg();
 

@@ -245,7 +245,7 @@ def test_propose_edge_cases(case, path):
 
 
 # forward paths: (kernel path, RoIs promised grouped by image)
-FWD_PATHS = [("dense", True), ("dense", False), ("generic", False)]
+FWD_PATHS = [("sorted", True), ("sorted", False), ("dense", True), ("dense", False), ("generic", False)]
 
 
 def _special_x(r, N=2, C=16, H=12, W=14):
@@ -313,21 +313,30 @@ def _rand_rois(r, b, H, W, lo=-3, span=40):
     return np.concatenate([np.asarray(b, np.float32)[:, None], xy, xy + wh], 1).astype(np.float32)
 
 
+@pytest.mark.parametrize("fpath", ["sorted", "dense"])
 @pytest.mark.parametrize("split", ["auto", "1", "3", "64"])
 @pytest.mark.parametrize("case", ["many_images", "invalid_ends", "unsorted", "single_roi", "gaps",
                                   "one_image_tiny_rois", "uniform_sizes", "ph5", "ph8x8", "ph3x9",
-                                  "cfg4_shape", "c8", "c4"])
-def test_roi_pool_dense_cases(case, split):
-    """The dense image-tile forward: cost-balanced shares (`split` per image),
-    geometry chunks, window-class ordering, bins packed across RoIs for any
-    PH x PW <= 64, out-of-range batch indices, 16 / 8 / 4-channel tiles, and any
-    RoI order (per-image lists) -- bit-exact vs the oracle."""
+                                  "cfg4_shape", "c8", "c4", "ph1_huge", "ph2_wide"])
+def test_roi_pool_tile_cases(case, split, fpath):
+    """The image-tile forwards (shape-sorted bins, and RoI-packed "dense"):
+    cost-balanced shares (`split` per image), geometry chunks, every window
+    shape class (dw 1-4 unrolled, 5-62 uniform loop, > 62 per-lane), any
+    PH x PW <= 64, out-of-range batch indices, 16 / 8 / 4-channel tiles, and
+    any RoI order (per-image lists) -- bit-exact vs the oracle."""
     r = np.random.default_rng(sum(map(ord, case)))
-    ph, pw = {"ph5": (5, 5), "ph8x8": (8, 8), "ph3x9": (3, 9)}.get(case, (7, 7))
+    ph, pw = {"ph5": (5, 5), "ph8x8": (8, 8), "ph3x9": (3, 9), "ph1_huge": (1, 1),
+              "ph2_wide": (2, 3)}.get(case, (7, 7))
     N, C, H, W = 4, 16, 20, 27
     span = 40
     sorted_ = case != "unsorted"
-    if case == "many_images":  # more images than one geometry chunk
+    if case == "ph1_huge":  # one bin = the whole RoI: windows up to 80 x 100 (> 62)
+        N, C, H, W, span = 2, 8, 80, 100, 110
+        b = np.sort(r.integers(0, N, 300))
+    elif case == "ph2_wide":
+        N, C, H, W, span = 2, 16, 30, 90, 80
+        b = np.sort(r.integers(0, N, 300))
+    elif case == "many_images":  # more images than one geometry chunk
         N, C, H, W, span = 20000, 8, 4, 5, 6
         b = np.sort(r.integers(0, N, 40000))
     elif case == "invalid_ends":
@@ -354,7 +363,7 @@ def test_roi_pool_dense_cases(case, split):
     rois = _rand_rois(r, b, H, W, span=span)
     if case == "uniform_sizes":
         rois[:, 3:] = rois[:, 1:3] + 6.0
-    with _lib.kernel_path("roi_pool_split", split):
+    with _lib.kernel_path("roi_pool_split", split), _lib.kernel_path("roi_pool_fwd", fpath):
         out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV),
                                            (ph, pw), rois_sorted=sorted_)
     oo, oa = orc.roi_pool_forward(x, rois, (ph, pw))

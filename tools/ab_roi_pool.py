@@ -1,10 +1,11 @@
 """A/B timing of the RoIPool forward paths on one device, interleaved rounds.
 
-    python tools/ab_roi_pool.py [--config cfg2] [--variants dense,dense@3,unsorted,generic]
+    python tools/ab_roi_pool.py [--config cfg2] [--variants sorted,sorted:8,dense@3,sorted/u,generic]
 
-`name@k` runs `name` with frcnn_set_path("roi_pool_split", k) (RoI shares per
-image).  Names: dense (RoIs promised grouped by image, one launch), unsorted
-(per-image lists first), generic (one workgroup per RoI).
+A variant is `path[:cg][@split][/u]`: path = sorted | dense | generic
+(frcnn_set_path("roi_pool_fwd", path)), cg = channels per workgroup
+("roi_pool_cg"), split = RoI / unit shares per image ("roi_pool_split"), /u =
+RoIs passed as unsorted (per-image lists first).
 
 Inputs are the bench's: the config's features + the proposals of the batch.
 Every variant's output is checked bit-equal to the first variant's.
@@ -26,7 +27,7 @@ from replication_faster_rcnn_amd import anchors as A  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg2")
-    ap.add_argument("--variants", default="dense,unsorted")
+    ap.add_argument("--variants", default="sorted,dense")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
@@ -48,14 +49,19 @@ def main():
     times = {v: [] for v in variants}
     for rnd in range(a.rounds):
         for vs in variants:
-            v, _, sp = vs.partition("@")
+            v, uns = (vs[:-2], True) if vs.endswith("/u") else (vs, False)
+            v, _, probe = v.partition("!")
+            v, _, sp = v.partition("@")
+            v, _, cg = v.partition(":")
+            _lib.set_path("roi_pool_probe", probe or "0")
             _lib.set_path("roi_pool_split", sp or "auto")
-            _lib.set_path("roi_pool_fwd", "generic" if v == "generic" else "auto")
-            srt = v == "dense"
+            _lib.set_path("roi_pool_cg", cg or "auto")
+            _lib.set_path("roi_pool_fwd", v)
+            srt = not uns
             out, am = ops._roi_pool_fwd(x, boxes, 7, 7, 1.0, srt)
             if ref is None:
                 ref = (out.clone(), am.clone())
-            elif rnd == 0:
+            elif rnd == 0 and not probe:
                 assert torch.equal(out, ref[0]) and torch.equal(am, ref[1]), f"variant {vs} differs"
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -64,8 +70,9 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             times[vs].append(e0.elapsed_time(e1) / a.iters * 1e3)
-    _lib.set_path("roi_pool_split", "auto")
-    _lib.set_path("roi_pool_fwd", "auto")
+    _lib.set_path("roi_pool_probe", "0")
+    for op in ("roi_pool_split", "roi_pool_cg", "roi_pool_fwd"):
+        _lib.set_path(op, "auto")
     res = {v: {"us_median": float(np.median(t)), "us_min": float(np.min(t)),
                "GBps": alg / (np.median(t) * 1e-6) / 1e9} for v, t in times.items()}
     print(json.dumps({"config": a.config, "R": R, "alg_bytes": alg, "variants": res}, indent=1))
