@@ -18,7 +18,8 @@ void set_error(const char* fmt, ...);
 constexpr int kPathAuto = 0;
 constexpr int kPathGeneric = 1;  // roi_pool_fwd: one workgroup per RoI
 constexpr int kPathDense = 2;    // roi_pool_fwd: image tile, RoI bins packed per wave
-constexpr int kPathSorted = 3;   // roi_pool_fwd: image tile, bins sorted by window shape
+constexpr int kPathSorted = 3;   // roi_pool_fwd: image tile, bins sorted by window shape per image
+constexpr int kPathStaged = 4;   // roi_pool_fwd: image tile, bins sorted per RoI block, LDS-staged output
 constexpr int kPathPlain = 1;    // roi_pool_bwd: the unpipelined plane-owner kernel
 constexpr int kPathHybrid = 1;   // propose: fused per image + chip-wide first-chunk mask
 constexpr int kPathLazy = 2;     // propose: fused per image, lazy NMS from the first chunk on

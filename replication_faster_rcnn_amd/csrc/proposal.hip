@@ -1,19 +1,18 @@
 // Proposal layer (nets/rpn.py:47-79) and torchvision-style NMS on gfx950.
 //
-// Pipeline, one launch each, batched over images (blockIdx.y / blockIdx.x = image):
-//   1. decode_filter  : anchors (generated in-register) + deltas -> decoded,
-//                       clamped boxes; min-size mask; 64-bit sort key
-//                       (desc score : anchor index) -- nets/rpn.py:58-68
-//   2. select         : wave64-ballot radix select of the pre_nms-th key, one
-//                       1024-thread workgroup per image -- nets/rpn.py:71-72
-//   3. compact        : keys <= threshold appended to a per-image list
-//   4. rank           : rank = #smaller keys (keys are unique), scatter boxes
-//                       into score order -- nets/rpn.py:71-74
-//   5. nms_mask       : 64x64 IoU tiles of the upper triangle -> bitmask,
-//                       stored column-block-major maskT[cb][i]
-//   6. nms_sweep      : greedy resolution per image, one workgroup; a wave
-//                       resolves each 64-box block serially in SGPRs; stops
-//                       as soon as post_nms boxes are kept -- nets/rpn.py:75-77
+// decode_filter: anchors (generated in-register) + deltas -> decoded, clamped
+// boxes; min-size mask; 64-bit sort key (desc score : anchor index) --
+// nets/rpn.py:58-68.  Then one of two paths, batched over images:
+//   fused (many images / small post_nms): one 1024-thread workgroup per image
+//     selects, sorts and suppresses 1024-candidate chunks on chip (below);
+//   wide (few images, large pre/post_nms: cfg1, cfg4, the nms op):
+//     run_sort + merge_rank + rank_scatter -- every key sorted chip-wide,
+//       the first min(#valid, pre_nms) ranks scattered in score order
+//       (nets/rpn.py:71-74);
+//     staged NMS -- column-form 64x64 IoU tiles of one stage of column
+//       blocks, then a resumable one-workgroup greedy sweep over those
+//       blocks; stages stop being built once post_nms boxes are kept
+//       (nets/rpn.py:75-77).
 // Ties in score are ordered by ascending anchor index (documented deviation:
 // the reference's CPU argsort is unstable under ties).
 #include <cfloat>
@@ -127,150 +126,138 @@ __global__ __launch_bounds__(256) void nms_keys_kernel(const float* __restrict__
     keys[i] = (static_cast<uint64_t>(desc_score_key(scores[i])) << 32) | static_cast<uint32_t>(i);
 }
 
-// ---------------------------------------------------------------- 2. select
-// One 1024-thread workgroup per image.  Finds T = the K-th smallest valid key
-// (K = min(#valid, pre)), MSB-first over 8-bit digits; per-digit histograms
-// are built with one LDS atomic per (wave, distinct digit) via ballots.
-__global__ __launch_bounds__(1024) void select_kernel(const uint64_t* __restrict__ keys_all, int A,
-                                                      int pre, uint64_t* __restrict__ sel_T,
-                                                      int* __restrict__ sel_P,
-                                                      unsigned* __restrict__ list_cnt) {
-    const int n = blockIdx.x;
-    const uint64_t* keys = keys_all + static_cast<size_t>(n) * A;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    __shared__ unsigned hist[256];
-    __shared__ unsigned s_part[16];
-    __shared__ unsigned s_digit, s_before, s_bucket;
+// ------------------------------------------------- 2-4. sort (wide path)
+// Every key of the image is sorted (no select pass): runs of 1024 keys are
+// sorted in LDS, each key's rank in every other run is one binary search in
+// that run (a workgroup per (run, run) pair, the searched run staged in LDS),
+// and the ranks are summed and scattered.  O(A log A) work spread over the
+// chip; the first min(#valid, pre_nms) ranks are the proposal layer's top-k
+// (nets/rpn.py:71-74).  Invalid (filtered) keys are made unique and sorted
+// after every valid key.
+constexpr int kRun = 1024;
 
-    unsigned c = 0;
-    for (int i = tid; i < A; i += 1024) c += keys[i] != kInvalidKey;
-    c = wave_sum_u32(c);
-    if (lane == 0) s_part[wid] = c;
+__device__ __forceinline__ uint64_t unique_key(uint64_t k, int a) {
+    return k == kInvalidKey ? ((~0ull << 32) | static_cast<uint32_t>(a)) : k;
+}
+
+// # of keys < k in the sorted run s[0, len)
+__device__ __forceinline__ int lower_bound_u64(const uint64_t* s, int len, uint64_t k) {
+    int lo = 0, n = len;
+    while (n > 0) {
+        const int h = n >> 1;
+        if (s[lo + h] < k) {
+            lo += h + 1;
+            n -= h + 1;
+        } else {
+            n = h;
+        }
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(1024) void run_sort_kernel(const uint64_t* __restrict__ keys_all, int A, int nr,
+                                                        uint64_t* __restrict__ runs_all, int* __restrict__ vcount) {
+    const int n = blockIdx.y, i = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int base = i * kRun;
+    const int len = min(kRun, A - base);
+    __shared__ uint64_t s[kRun];
+    __shared__ int s_v[16];
+    const uint64_t raw = tid < len ? keys_all[static_cast<size_t>(n) * A + base + tid] : kInvalidKey;
+    uint64_t key = tid < len ? unique_key(raw, base + tid) : ~0ull;
+    const uint64_t vb = __ballot(tid < len && raw != kInvalidKey);
+    if (lane == 0) s_v[wid] = __popcll(vb);
+    for (int kk = 2; kk <= 64; kk <<= 1) {  // bitonic sort of the wave's 64 keys
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            const uint64_t other = __shfl_xor(key, j, 64);
+            const bool asc = (lane & kk) == 0;
+            const bool lower = (lane & j) == 0;
+            const uint64_t mn = other < key ? other : key;
+            const uint64_t mx = other < key ? key : other;
+            key = (lower == asc) ? mn : mx;
+        }
+    }
+    s[tid] = key;
     __syncthreads();
-    unsigned M = 0;
-    for (int w = 0; w < 16; ++w) M += s_part[w];
-    const unsigned Kc = M < static_cast<unsigned>(pre) ? M : static_cast<unsigned>(pre);
+    int rank = lane;
+#pragma unroll 1
+    for (int w = 0; w < 16; ++w)
+        if (w != wid) rank += lower_bound_u64(s + 64 * w, 64, key);
     if (tid == 0) {
-        list_cnt[n] = 0;
-        sel_P[n] = static_cast<int>(Kc);
+        int v = 0;
+        for (int w = 0; w < 16; ++w) v += s_v[w];
+        vcount[n * nr + i] = v;
     }
-    if (Kc == M) {  // everything valid is selected
-        if (tid == 0) sel_T[n] = kInvalidKey - 1;
-        return;
-    }
-    uint64_t prefix = 0;
-    unsigned need = Kc;
-    uint64_t T = 0;
-    for (int shift = 56; shift >= 0; shift -= 8) {
-        if (tid < 256) hist[tid] = 0;
-        __syncthreads();
-        const uint64_t himask = shift == 56 ? 0ull : (~0ull << (shift + 8));
-        for (int i0 = 0; i0 < A; i0 += 1024) {
-            int i = i0 + tid;
-            uint64_t k = i < A ? keys[i] : kInvalidKey;
-            bool m = k != kInvalidKey && (k & himask) == prefix;
-            unsigned d = static_cast<unsigned>(k >> shift) & 255u;
-            uint64_t act = __ballot(m);
-            while (act) {
-                int leader = __ffsll(static_cast<unsigned long long>(act)) - 1;
-                unsigned dl = __builtin_amdgcn_readlane(d, leader);
-                uint64_t same = __ballot(m && d == dl);
-                if (lane == leader) atomicAdd(&hist[dl], static_cast<unsigned>(__popcll(same)));
-                act &= ~same;
-            }
-        }
-        __syncthreads();
-        if (wid == 0) {
-            unsigned h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2],
-                     h3 = hist[4 * lane + 3];
-            unsigned tot = h0 + h1 + h2 + h3;
-            unsigned incl = tot;  // inclusive wave scan
-            for (int o = 1; o < 64; o <<= 1) {
-                unsigned v = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += v;
-            }
-            unsigned before = incl - tot;
-            unsigned hv[4] = {h0, h1, h2, h3};
-            for (int q = 0; q < 4; ++q) {
-                if (before < need && before + hv[q] >= need) {
-                    s_digit = 4 * lane + q;
-                    s_before = before;
-                    s_bucket = hv[q];
-                }
-                before += hv[q];
-            }
-        }
-        __syncthreads();
-        unsigned d = s_digit;
-        need -= s_before;
-        prefix |= static_cast<uint64_t>(d) << shift;
-        if (s_bucket == need) {  // the whole bucket is taken
-            T = prefix | ((1ull << shift) - 1ull);
-            break;
-        }
-        __syncthreads();
-    }
-    if (tid == 0) sel_T[n] = T;
-}
-
-// --------------------------------------------------------------- 3. compact
-__global__ __launch_bounds__(256) void compact_kernel(const uint64_t* __restrict__ keys_all, int A,
-                                                      int pre, const uint64_t* __restrict__ sel_T,
-                                                      unsigned* __restrict__ list_cnt,
-                                                      uint64_t* __restrict__ list_keys) {
-    const int n = blockIdx.y;
-    const int a = blockIdx.x * 256 + threadIdx.x;
-    const uint64_t T = sel_T[n];
-    uint64_t k = a < A ? keys_all[static_cast<size_t>(n) * A + a] : kInvalidKey;
-    bool m = k != kInvalidKey && k <= T;
-    uint64_t act = __ballot(m);
-    if (!act) return;
-    int leader = __ffsll(static_cast<unsigned long long>(act)) - 1;
-    unsigned base = 0;
-    if (lane_id() == leader) base = atomicAdd(&list_cnt[n], static_cast<unsigned>(__popcll(act)));
-    base = __shfl(base, leader, 64);
-    if (m) list_keys[static_cast<size_t>(n) * pre + base + __popcll(act & lanemask_lt())] = k;
-}
-
-// ------------------------------------------------------------------ 4. rank
-// 64 candidates per workgroup, the 4 waves split the comparison range.
-__global__ __launch_bounds__(256) void rank_kernel(const uint64_t* __restrict__ list_keys, int pre,
-                                                   const int* __restrict__ sel_P,
-                                                   const float4* __restrict__ box_src, int A,
-                                                   float4* __restrict__ sbox,
-                                                   int32_t* __restrict__ sidx) {
-    const int n = blockIdx.y;
-    const int P = sel_P[n];
-    const int i0 = blockIdx.x * 64;
-    if (i0 >= P) return;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint64_t* lk = list_keys + static_cast<size_t>(n) * pre;
-    __shared__ uint64_t tile[1024];
-    __shared__ unsigned part[4][64];
-    const int i = i0 + lane;
-    const uint64_t ki = i < P ? lk[i] : kInvalidKey;
-    unsigned cnt = 0;
-    for (int t0 = 0; t0 < P; t0 += 1024) {
-        for (int q = tid; q < 1024; q += 256) tile[q] = (t0 + q < P) ? lk[t0 + q] : kInvalidKey;
-        __syncthreads();
-        const uint64_t* tw = tile + wid * 256;
-#pragma unroll 8
-        for (int j = 0; j < 256; ++j) cnt += tw[j] < ki;
-        __syncthreads();
-    }
-    part[wid][lane] = cnt;
     __syncthreads();
-    if (wid == 0 && i < P) {
-        unsigned r = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
-        uint32_t a = static_cast<uint32_t>(ki);
-        sidx[static_cast<size_t>(n) * pre + r] = static_cast<int32_t>(a);
-        sbox[static_cast<size_t>(n) * pre + r] = box_src[static_cast<size_t>(n) * A + a];
+    if (key != ~0ull) s[rank] = key;  // the padding (~0) is never placed
+    __syncthreads();
+    if (tid < len) runs_all[static_cast<size_t>(n) * nr * kRun + base + tid] = s[tid];
+}
+
+// Workgroup (i, j): for every key of run i, the number of keys of run j below it.
+__global__ __launch_bounds__(1024) void merge_rank_kernel(const uint64_t* __restrict__ runs_all, int A, int nr,
+                                                          int* __restrict__ part) {
+    const int n = blockIdx.z, j = blockIdx.y, i = blockIdx.x;
+    if (i == j) return;
+    const int tid = threadIdx.x;
+    const int leni = min(kRun, A - i * kRun), lenj = min(kRun, A - j * kRun);
+    const uint64_t* runs = runs_all + static_cast<size_t>(n) * nr * kRun;
+    __shared__ uint64_t s[kRun];
+    if (tid < lenj) s[tid] = runs[j * kRun + tid];
+    __syncthreads();
+    if (tid < leni)
+        part[(static_cast<size_t>(n) * nr + j) * nr * kRun + i * kRun + tid] =
+            lower_bound_u64(s, lenj, runs[i * kRun + tid]);
+}
+
+// Per-image state of the staged NMS (carried from one stage launch to the next).
+struct SweepState {
+    int* count;      // [N] boxes kept so far
+    int* done;       // [N] post_nms reached or every candidate examined
+    uint64_t* kept;  // [N][Wc] kept bits of each 64-candidate block
+};
+
+__global__ __launch_bounds__(1024) void rank_scatter_kernel(const uint64_t* __restrict__ runs_all,
+                                                            const int* __restrict__ part,
+                                                            const int* __restrict__ vcount, int A, int nr,
+                                                            int pre, const float4* __restrict__ box_src,
+                                                            float4* __restrict__ sbox, int32_t* __restrict__ sidx,
+                                                            int* __restrict__ sel_P, SweepState ss) {
+    const int n = blockIdx.y, i = blockIdx.x;
+    const int tid = threadIdx.x;
+    int nvalid = 0;
+    for (int j = 0; j < nr; ++j) nvalid += vcount[n * nr + j];
+    const int P = nvalid < pre ? nvalid : pre;
+    if (i == 0 && tid == 0) {
+        sel_P[n] = P;
+        ss.count[n] = 0;
+        ss.done[n] = 0;
+    }
+    const int len = min(kRun, A - i * kRun);
+    if (tid >= len) return;
+    const uint64_t key = runs_all[static_cast<size_t>(n) * nr * kRun + i * kRun + tid];
+    int rank = tid;
+    const int* pp = part + static_cast<size_t>(n) * nr * nr * kRun + i * kRun + tid;
+#pragma unroll 8
+    for (int j = 0; j < nr; ++j)  // independent loads: unrolled so they are in flight together
+        rank += j != i ? pp[static_cast<size_t>(j) * nr * kRun] : 0;
+    if (rank < P) {
+        const uint32_t a = static_cast<uint32_t>(key);
+        sidx[static_cast<size_t>(n) * pre + rank] = static_cast<int32_t>(a);
+        sbox[static_cast<size_t>(n) * pre + rank] = box_src[static_cast<size_t>(n) * A + a];
     }
 }
 
-// -------------------------------------------------------------- 5. nms mask
-// Upper-triangle tile t -> (row block rb, col block cb >= rb).
-__device__ __forceinline__ void tri_tile(int t, int nb, int& rb, int& cb) {
+// ------------------------------------------------- 5-6. staged NMS (wide)
+// The candidates are resolved in stages of column blocks [cb0, cb1) (64
+// candidates each; stage widths 32, 64, 128, ... blocks).  A stage computes
+// the IoU bits of its columns against every earlier row (64x64 tiles, upper
+// triangle, chip-wide), then one workgroup per image continues the greedy
+// sweep over the stage's blocks.  An image that has kept post_nms boxes (or
+// run out of candidates) is marked done and every later stage returns at
+// once, so the O(pre^2) triangle is only built as far as the sweep needs it
+// (cfg4: ~2,600 of 30,000 rows).
+__device__ __forceinline__ void tri_tile(int t, int nb, int& rb, int& cb) {  // full triangle (fused path)
     int total = nb * (nb + 1) / 2;
     int tr = total - 1 - t;  // reversed: row lengths 1, 2, 3, ...
     int r = static_cast<int>((sqrt(8.0 * tr + 1.0) - 1.0) * 0.5);
@@ -281,108 +268,179 @@ __device__ __forceinline__ void tri_tile(int t, int nb, int& rb, int& cb) {
     cb = nb - 1 - off;
 }
 
-__global__ __launch_bounds__(64) void nms_mask_kernel(const float4* __restrict__ sbox_all, int pre,
-                                                      int Wc, const int* __restrict__ sel_P,
-                                                      NmsThr thr, uint64_t* __restrict__ maskT) {
-    const int n = blockIdx.y;
-    const int P = sel_P[n];
-    const int nbP = (P + 63) / 64;
-    int rb, cb;
-    tri_tile(blockIdx.x, Wc, rb, cb);
-    if (rb >= nbP || cb >= nbP) return;
-    const float4* sbox = sbox_all + static_cast<size_t>(n) * pre;
-    const int lane = threadIdx.x;
-    __shared__ float4 cbox[64];
-    __shared__ float carea[64];
-    const int j = cb * 64 + lane;
-    if (j < P) {
-        float4 b = sbox[j];
-        cbox[lane] = b;
-        carea[lane] = box_area(b);
-    }
-    __syncthreads();
-    const int i = rb * 64 + lane;
-    if (i >= P) return;
-    uint64_t bits = 0;
-    if (!thr.never) {
-        float4 bi = sbox[i];
-        float ai = box_area(bi);
-        int jend = P - cb * 64;
-        jend = jend < 64 ? jend : 64;
-        int jstart = rb == cb ? lane + 1 : 0;
-        for (int jj = jstart; jj < jend; ++jj)
-            if (iou_over(bi, ai, cbox[jj], carea[jj], thr)) bits |= 1ull << jj;
-    }
-    maskT[(static_cast<size_t>(n) * Wc + cb) * pre + i] = bits;
+// Tile t of the stage starting at column block cb0: columns in order, rows 0..cb.
+__device__ __forceinline__ void stage_tile(int t, int cb0, int& rb, int& cb) {
+    const int64_t u = static_cast<int64_t>(t) + static_cast<int64_t>(cb0) * (cb0 + 1) / 2;
+    int c = static_cast<int>((sqrt(8.0 * static_cast<double>(u) + 1.0) - 1.0) * 0.5);
+    while (static_cast<int64_t>(c + 1) * (c + 2) / 2 <= u) ++c;
+    while (static_cast<int64_t>(c) * (c + 1) / 2 > u) --c;
+    cb = c;
+    rb = static_cast<int>(u - static_cast<int64_t>(c) * (c + 1) / 2);
 }
 
-// ------------------------------------------------------------- 6. nms sweep
+// Column form: maskC[n][cb][rb][lane] bit i = row 64*rb + i suppresses column
+// 64*cb + lane (torchvision's IoU test, rows before the column only), so the
+// sweep turns a kept-row set into removed columns with one ballot per tile.
+// 256 threads per tile: lane = column, wave w tests rows [16w, 16w+16) of the
+// row block (4 independent waves per tile keep the SIMDs busy), the four
+// partial words are OR-ed in LDS.  The grid is capped (workgroups stride over
+// the stage's tiles), so a stage of a finished image costs one short launch.
+constexpr int kMaskGrid = 2048;
+
+__global__ __launch_bounds__(256) void nms_mask_stage_kernel(const float4* __restrict__ sbox_all, int pre,
+                                                             int Wc, const int* __restrict__ sel_P,
+                                                             const int* __restrict__ done, int cb0,
+                                                             int ntiles, NmsThr thr,
+                                                             uint64_t* __restrict__ maskC) {
+    const int n = blockIdx.y;
+    if (done[n]) return;
+    const int P = sel_P[n];
+    const int nbP = (P + 63) / 64;
+    const float4* sbox = sbox_all + static_cast<size_t>(n) * pre;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    __shared__ float4 rbox[64];
+    __shared__ float rarea[64];
+    __shared__ uint64_t part[4][64];
+    for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        int rb, cb;
+        stage_tile(t, cb0, rb, cb);
+        if (cb >= nbP) break;  // tiles go by column: the rest are past the candidates too
+        if (rb >= nbP) continue;
+        const int i0 = rb * 64;
+        __syncthreads();  // the previous tile is done with rbox / part
+        if (tid < 64 && i0 + tid < P) {
+            const float4 b = sbox[i0 + tid];
+            rbox[tid] = b;
+            rarea[tid] = box_area(b);
+        }
+        const int j = cb * 64 + lane;
+        const bool jv = j < P;
+        const float4 bj = jv ? sbox[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float aj = box_area(bj);
+        __syncthreads();
+        int iend = min(64, P - i0);
+        if (rb == cb) iend = min(iend, lane);  // rows before the column
+        if (!jv) iend = 0;
+        uint64_t bits = 0;
+        if (!thr.never) {
+            const int r0 = wid * 16;
+#pragma unroll 4
+            for (int ii = r0; ii < r0 + 16; ++ii)
+                if (ii < iend && iou_over(rbox[ii], rarea[ii], bj, aj, thr)) bits |= 1ull << ii;
+        }
+        part[wid][lane] = bits;
+        __syncthreads();
+        if (wid == 0 && jv)
+            maskC[((static_cast<size_t>(n) * Wc + cb) * Wc + rb) * 64 + lane] =
+                part[0][lane] | part[1][lane] | part[2][lane] | part[3][lane];
+    }
+}
+
+// One 1024-thread workgroup per image continues the greedy sweep over the
+// stage's blocks [cb0, cb1), 16 blocks (1024 candidates) at a time: wave w owns
+// column block sb0 + w, lane = column.  Each lane first ORs in the kept rows of
+// every earlier block (one round of independent loads), then holds the
+// column-form words of the sub-stage's earlier blocks in registers, so the
+// sub-stage resolves block after block with one barrier each and no memory
+// latency: wave q computes avail = ~hit, runs the fixed point
+// K <- avail & ballot(diag & K == 0) (unique, = the greedy result), and the
+// later waves fold K into their hit flags.
 // OUT_MODE 0: propose outputs (boxes + int32 anchor index, zero padding);
 // OUT_MODE 1: nms op output (int64 index into the original box array).
+constexpr int kSub = 16;  // blocks per sub-stage (= waves of the workgroup)
+
 template <int OUT_MODE>
-__global__ __launch_bounds__(256) void nms_sweep_kernel(
-    const uint64_t* __restrict__ maskT_all, const float4* __restrict__ sbox_all,
-    const int32_t* __restrict__ sidx_all, int pre, int Wc, const int* __restrict__ sel_P,
-    int post, float4* __restrict__ out_rois, int32_t* __restrict__ out_idx,
+__global__ __launch_bounds__(1024) void nms_sweep_stage_kernel(
+    const uint64_t* __restrict__ maskC_all, const float4* __restrict__ sbox_all,
+    const int32_t* __restrict__ sidx_all, int pre, int Wc, const int* __restrict__ sel_P, int post,
+    int cb0, int cb1, SweepState ss, float4* __restrict__ out_rois, int32_t* __restrict__ out_idx,
     int64_t* __restrict__ out_keep, int32_t* __restrict__ out_count) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t kept_bits[];  // [Wc]
-    __shared__ uint64_t red[4];
-    __shared__ int s_count;
+    extern __shared__ __attribute__((aligned(16))) uint64_t kept[];  // [Wc]
+    __shared__ uint64_t s_K[2];
+    __shared__ int s_count[2];
     const int n = blockIdx.x;
+    if (ss.done[n]) return;  // uniform
     const int P = sel_P[n];
     const int nb = (P + 63) / 64;
+    const int end = min(cb1, nb);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint64_t* maskT = maskT_all + static_cast<size_t>(n) * Wc * pre;
+    const uint64_t* maskC = maskC_all + static_cast<size_t>(n) * Wc * Wc * 64;
     const float4* sbox = sbox_all + static_cast<size_t>(n) * pre;
     const int32_t* sidx = sidx_all + static_cast<size_t>(n) * pre;
-    if (tid == 0) s_count = 0;
+    uint64_t* gkept = ss.kept + static_cast<size_t>(n) * Wc;
+    int count = ss.count[n];
+    for (int b = tid; b < cb0; b += 1024) kept[b] = gkept[b];
     __syncthreads();
-    int count = 0;
-    for (int b = 0; b < nb && count < post; ++b) {
-        const uint64_t* col = maskT + static_cast<size_t>(b) * pre;
-        uint64_t acc = 0;
-        for (int i = tid; i < 64 * b; i += 256)
-            if ((kept_bits[i >> 6] >> (i & 63)) & 1ull) acc |= col[i];
-        acc = wave_or_u64(acc);
-        if (lane == 0) red[wid] = acc;
-        __syncthreads();
-        if (wid == 0) {
-            uint64_t removed = red[0] | red[1] | red[2] | red[3];
-            int rows = P - 64 * b;
-            if (rows < 64) removed |= ~0ull << rows;
-            uint64_t diag = lane < rows ? col[64 * b + lane] : 0ull;
-            uint64_t avail = ~removed;
-            uint64_t kept = 0;
-            int cnt = count;
-            while (avail && cnt < post) {
-                int l = __builtin_amdgcn_readfirstlane(__ffsll(static_cast<unsigned long long>(avail)) - 1);
-                kept |= 1ull << l;
-                ++cnt;
-                avail &= ~(readlane_u64(diag, l) | (1ull << l));
-            }
-            if (lane == 0) kept_bits[b] = kept;
-            if ((kept >> lane) & 1ull) {
-                int slot = count + __popcll(kept & lanemask_lt());
-                int r = 64 * b + lane;
-                if (OUT_MODE == 0) {
-                    out_rois[static_cast<size_t>(n) * post + slot] = sbox[r];
-                    out_idx[static_cast<size_t>(n) * post + slot] = sidx[r];
-                } else {
-                    out_keep[slot] = sidx[r];
+    for (int sb0 = cb0; sb0 < end && count < post; sb0 += kSub) {
+        const int nsb = min(kSub, end - sb0);
+        const int cb = sb0 + wid;  // this wave's column block
+        const bool mine = wid < nsb;
+        const int j = 64 * cb + lane;
+        const uint64_t* colw = maskC + static_cast<size_t>(cb) * Wc * 64 + lane;  // tile (cb, rb) at colw[rb*64]
+        bool hit = false;
+        uint64_t col[kSub];
+        float4 bxj = make_float4(0.f, 0.f, 0.f, 0.f);
+        int32_t sj = -1;
+        if (mine && j < P) {  // the outputs' data, loaded before the serial part
+            bxj = sbox[j];
+            sj = sidx[j];
+        }
+        if (mine) {
+            for (int rb = 0; rb < sb0; ++rb) hit |= (colw[static_cast<size_t>(rb) * 64] & kept[rb]) != 0ull;
+#pragma unroll
+            for (int q = 0; q < kSub; ++q) col[q] = q <= wid ? colw[static_cast<size_t>(sb0 + q) * 64] : 0ull;
+        }
+#pragma unroll
+        for (int q = 0; q < kSub; ++q) {
+            if (q >= nsb || count >= post) break;  // uniform
+            if (wid == q) {
+                const uint64_t avail = __ballot(j < P && !hit);
+                const uint64_t diag = col[q];
+                uint64_t K = avail;
+                for (int it = 0; it < 65; ++it) {
+                    const uint64_t Kn = avail & __ballot((diag & K) == 0ull);
+                    if (Kn == K) break;
+                    K = Kn;
+                }
+                const int room = post - count;
+                while (__popcll(K) > room) K &= ~(1ull << (63 - __clzll(K)));  // keep the first `room`
+                if ((K >> lane) & 1ull) {
+                    const int slot_i = count + __popcll(K & lanemask_lt());
+                    if (OUT_MODE == 0) {
+                        out_rois[static_cast<size_t>(n) * post + slot_i] = bxj;
+                        out_idx[static_cast<size_t>(n) * post + slot_i] = sj;
+                    } else {
+                        out_keep[slot_i] = sj;
+                    }
+                }
+                if (lane == 0) {
+                    kept[cb] = K;
+                    s_K[q & 1] = K;
+                    s_count[q & 1] = count + __popcll(K);
                 }
             }
-            if (lane == 0) s_count = cnt;
+            __syncthreads();
+            const uint64_t K = s_K[q & 1];
+            count = s_count[q & 1];
+            if (wid > q && (col[q] & K) != 0ull) hit = true;
         }
-        __syncthreads();
-        count = s_count;
+        __syncthreads();  // kept[] of this sub-stage complete before the next one's loads
     }
-    if (OUT_MODE == 0) {
-        for (int s = count + tid; s < post; s += 256) {
-            out_rois[static_cast<size_t>(n) * post + s] = make_float4(0.f, 0.f, 0.f, 0.f);
-            out_idx[static_cast<size_t>(n) * post + s] = -1;
+    const bool fin = count >= post || end >= nb;
+    if (fin) {
+        if (OUT_MODE == 0)
+            for (int s = count + tid; s < post; s += 1024) {
+                out_rois[static_cast<size_t>(n) * post + s] = make_float4(0.f, 0.f, 0.f, 0.f);
+                out_idx[static_cast<size_t>(n) * post + s] = -1;
+            }
+        if (tid == 0) {
+            out_count[n] = count;
+            ss.done[n] = 1;
         }
+    } else {
+        for (int b = cb0 + tid; b < end; b += 1024) gkept[b] = kept[b];
+        if (tid == 0) ss.count[n] = count;
     }
-    if (tid == 0) out_count[n] = count;
 }
 
 // ==================================================== fused per-image path
@@ -863,13 +921,14 @@ static bool use_fused(int N, int A, int post) {
 struct ProposeWs {
     uint64_t* keys;
     float4* boxes;
-    uint64_t* sel_T;
-    int* sel_P;
-    unsigned* list_cnt;
-    uint64_t* list_keys;
-    float4* sbox;
+    uint64_t* runs;   // [N][nr * kRun] sorted runs
+    int* part;        // [N][nr][nr * kRun] cross-run ranks
+    int* vcount;      // [N][nr] valid keys per run
+    int* sel_P;       // [N] min(#valid, pre)
+    float4* sbox;     // [N][pre] candidates in score order
     int32_t* sidx;
-    uint64_t* maskT;
+    uint64_t* maskC;  // [N][Wc][Wc][64] column-form IoU tiles (built stage by stage)
+    SweepState ss;
     HybWs hyb;
     size_t bytes;
 };
@@ -878,15 +937,19 @@ static ProposeWs carve(void* ws, int N, int A, int pre, bool need_boxes) {
     Carver c(ws);
     ProposeWs w{};
     const int Wc = (pre + 63) / 64;
+    const int nr = (A + kRun - 1) / kRun;
     w.keys = c.take<uint64_t>(static_cast<size_t>(N) * A);
     w.boxes = need_boxes ? c.take<float4>(static_cast<size_t>(N) * A) : nullptr;
-    w.sel_T = c.take<uint64_t>(N);
+    w.runs = c.take<uint64_t>(static_cast<size_t>(N) * nr * kRun);
+    w.part = c.take<int>(static_cast<size_t>(N) * nr * nr * kRun);
+    w.vcount = c.take<int>(static_cast<size_t>(N) * nr);
     w.sel_P = c.take<int>(N);
-    w.list_cnt = c.take<unsigned>(N);
-    w.list_keys = c.take<uint64_t>(static_cast<size_t>(N) * pre);
     w.sbox = c.take<float4>(static_cast<size_t>(N) * pre);
     w.sidx = c.take<int32_t>(static_cast<size_t>(N) * pre);
-    w.maskT = c.take<uint64_t>(static_cast<size_t>(N) * Wc * pre);
+    w.maskC = c.take<uint64_t>(static_cast<size_t>(N) * Wc * Wc * 64);
+    w.ss.count = c.take<int>(N);
+    w.ss.done = c.take<int>(N);
+    w.ss.kept = c.take<uint64_t>(static_cast<size_t>(N) * Wc);
     w.hyb.cbox = c.take<float4>(static_cast<size_t>(N) * kChunk);
     w.hyb.ckey = c.take<uint64_t>(static_cast<size_t>(N) * kChunk);
     w.hyb.cc = c.take<int>(N);
@@ -896,34 +959,42 @@ static ProposeWs carve(void* ws, int N, int A, int pre, bool need_boxes) {
     return w;
 }
 
-// steps 2-6, shared by frcnn_propose and frcnn_nms
+// Sort + staged NMS, shared by frcnn_propose (wide path) and frcnn_nms.
 static int sort_and_suppress(const ProposeWs& w, const float4* box_src, int N, int A, int pre,
                              int post, double iou_thr, int out_mode, float4* out_rois,
                              int32_t* out_idx, int64_t* out_keep, int32_t* out_count,
                              hipStream_t st) {
     const int Wc = (pre + 63) / 64;
-    hipLaunchKernelGGL(select_kernel, dim3(N), dim3(1024), 0, st, w.keys, A, pre, w.sel_T, w.sel_P,
-                       w.list_cnt);
-    FRCNN_LAUNCH_CHECK("select_kernel");
-    hipLaunchKernelGGL(compact_kernel, dim3((A + 255) / 256, N), dim3(256), 0, st, w.keys, A, pre,
-                       w.sel_T, w.list_cnt, w.list_keys);
-    FRCNN_LAUNCH_CHECK("compact_kernel");
-    hipLaunchKernelGGL(rank_kernel, dim3(Wc, N), dim3(256), 0, st, w.list_keys, pre, w.sel_P,
-                       box_src, A, w.sbox, w.sidx);
-    FRCNN_LAUNCH_CHECK("rank_kernel");
+    const int nr = (A + kRun - 1) / kRun;
+    hipLaunchKernelGGL(run_sort_kernel, dim3(nr, N), dim3(1024), 0, st, w.keys, A, nr, w.runs, w.vcount);
+    FRCNN_LAUNCH_CHECK("run_sort_kernel");
+    if (nr > 1) {
+        hipLaunchKernelGGL(merge_rank_kernel, dim3(nr, nr, N), dim3(1024), 0, st, w.runs, A, nr, w.part);
+        FRCNN_LAUNCH_CHECK("merge_rank_kernel");
+    }
+    hipLaunchKernelGGL(rank_scatter_kernel, dim3(nr, N), dim3(1024), 0, st, w.runs, w.part, w.vcount, A, nr,
+                       pre, box_src, w.sbox, w.sidx, w.sel_P, w.ss);
+    FRCNN_LAUNCH_CHECK("rank_scatter_kernel");
     const NmsThr thr = make_thr(iou_thr);
-    const unsigned tiles = static_cast<unsigned>(Wc) * (Wc + 1) / 2;
-    hipLaunchKernelGGL(nms_mask_kernel, dim3(tiles, N), dim3(64), 0, st, w.sbox, pre, Wc, w.sel_P,
-                       thr, w.maskT);
-    FRCNN_LAUNCH_CHECK("nms_mask_kernel");
-    const size_t lds = static_cast<size_t>(Wc) * sizeof(uint64_t);
-    if (out_mode == 0)
-        hipLaunchKernelGGL(nms_sweep_kernel<0>, dim3(N), dim3(256), lds, st, w.maskT, w.sbox,
-                           w.sidx, pre, Wc, w.sel_P, post, out_rois, out_idx, out_keep, out_count);
-    else
-        hipLaunchKernelGGL(nms_sweep_kernel<1>, dim3(N), dim3(256), lds, st, w.maskT, w.sbox,
-                           w.sidx, pre, Wc, w.sel_P, post, out_rois, out_idx, out_keep, out_count);
-    FRCNN_LAUNCH_CHECK("nms_sweep_kernel");
+    // stage widths 48, 64, 128, ... blocks of 64 candidates (cfg4 needs 41
+    // blocks for post_nms = 2000, cfg1 92): every later stage of an image that
+    // is done returns at once
+    for (int cb0 = 0, width = 48; cb0 < Wc; cb0 += width, width = cb0 == 48 ? 64 : 2 * width) {
+        const int cb1 = cb0 + width < Wc ? cb0 + width : Wc;
+        const int64_t tiles = static_cast<int64_t>(cb1) * (cb1 + 1) / 2 - static_cast<int64_t>(cb0) * (cb0 + 1) / 2;
+        const unsigned grid = static_cast<unsigned>(tiles < kMaskGrid ? tiles : kMaskGrid);
+        hipLaunchKernelGGL(nms_mask_stage_kernel, dim3(grid, N), dim3(256), 0, st, w.sbox, pre, Wc, w.sel_P,
+                           w.ss.done, cb0, static_cast<int>(tiles), thr, w.maskC);
+        FRCNN_LAUNCH_CHECK("nms_mask_stage_kernel");
+        const size_t lds = static_cast<size_t>(Wc) * sizeof(uint64_t);
+        if (out_mode == 0)
+            hipLaunchKernelGGL(nms_sweep_stage_kernel<0>, dim3(N), dim3(1024), lds, st, w.maskC, w.sbox, w.sidx,
+                               pre, Wc, w.sel_P, post, cb0, cb1, w.ss, out_rois, out_idx, out_keep, out_count);
+        else
+            hipLaunchKernelGGL(nms_sweep_stage_kernel<1>, dim3(N), dim3(1024), lds, st, w.maskC, w.sbox, w.sidx,
+                               pre, Wc, w.sel_P, post, cb0, cb1, w.ss, out_rois, out_idx, out_keep, out_count);
+        FRCNN_LAUNCH_CHECK("nms_sweep_stage_kernel");
+    }
     return FRCNN_OK;
 }
 
@@ -937,6 +1008,7 @@ static int check_params(const frcnn_propose_params* p) {
     FRCNN_REQUIRE(p->A > 0, "frcnn_propose: A must be > 0");
     FRCNN_REQUIRE(p->pre_nms > 0 && p->post_nms > 0, "frcnn_propose: pre/post_nms must be > 0");
     FRCNN_REQUIRE(static_cast<int64_t>(p->pre_nms) <= (1 << 20), "frcnn_propose: pre_nms > 2^20");
+    FRCNN_REQUIRE(p->A <= (1 << 18), "frcnn_propose: A > 2^18");
     return FRCNN_OK;
 }
 
@@ -979,15 +1051,17 @@ extern "C" int frcnn_propose(const frcnn_propose_params* p, const float* scores,
                              reinterpret_cast<float4*>(out_rois), out_idx, nullptr, out_count, st);
 }
 
+constexpr int64_t kNmsMax = 1 << 16;  // bitmask workspace n * n / 8 B (512 MB at the cap)
+
 extern "C" size_t frcnn_nms_workspace_size(int64_t n) {
-    if (n <= 0 || n > (1 << 20)) return 0;
+    if (n <= 0 || n > kNmsMax) return 0;
     return carve(nullptr, 1, static_cast<int>(n), static_cast<int>(n), false).bytes;
 }
 
 extern "C" int frcnn_nms(const float* boxes, const float* scores, int64_t n, double iou_threshold,
                          int64_t* keep, int32_t* count, void* workspace, size_t ws_bytes,
                          void* stream) {
-    FRCNN_REQUIRE(n >= 0 && n <= (1 << 20), "frcnn_nms: n must be in [0, 2^20]");
+    FRCNN_REQUIRE(n >= 0 && n <= kNmsMax, "frcnn_nms: n must be in [0, 65536]");
     FRCNN_REQUIRE(count, "frcnn_nms: null count");
     hipStream_t st = as_stream(stream);
     if (n == 0) {

@@ -432,10 +432,13 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_dense_kernel(
             if (lane == 0) fn = atomicAdd(&s_misc[40], 64);  // prefetch the next chunk
             const int f = f0 + lane;
             const bool live = f < total;
+            // (the magic reciprocal of 1 wraps to 0: divisors of 1 bypass it)
             const int t = FIX ? (live ? f / PHW : 0)
-                              : (live ? static_cast<int>(__umulhi(static_cast<uint32_t>(f), magic_phw)) : 0);
+                              : (live ? (PHW == 1 ? f : static_cast<int>(__umulhi(static_cast<uint32_t>(f), magic_phw)))
+                                      : 0);
             const int k = f - t * PHW;
-            const int ph = FIX ? k / PW : static_cast<int>(__umulhi(static_cast<uint32_t>(k), magic_pw));
+            const int ph = FIX ? k / PW
+                               : (PW == 1 ? k : static_cast<int>(__umulhi(static_cast<uint32_t>(k), magic_pw)));
             const int pw = k - ph * PW;
             const int item = s_ord[t];
             const int4 gq = s_geo[item];
@@ -934,6 +937,311 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_sorted_kernel(
     }
 }
 
+// ------------------------------------------------- block-sorted forward
+// The default forward.  A workgroup owns CG channel planes of one image
+// (staged once into LDS, NaN -> -inf) and a contiguous share of that image's
+// RoIs, taken RB RoIs (a "block") at a time:
+//   1. the block's RB*PH*PW bins are counting-sorted by window shape
+//      (dh, dw) -- wave ballots rank equal shapes, one LDS atomic per
+//      (wave, shape) -- and cut into units of <= 64 bins of ONE shape,
+//      largest shapes first;
+//   2. waves pull units: the window walk is wave-uniform (scalar loop
+//      control, dw <= 4 fully unrolled with LDS immediates, no lane runs past
+//      its own window -- a RoI-per-wave mapping runs every lane for the RoI's
+//      largest window, 1.5x the pixels on VOC-shaped RoIs, and leaves 15 of 64
+//      lanes idle) and write their (max, argmax) pairs into an LDS staging
+//      image of the block's outputs;
+//   3. the block's outputs leave as contiguous 16-B stores: RoI r's channels
+//      [c0, c0+CG) x PH*PW are one run of out / argmax.
+// Window sizes > 15 fall back to per-lane walks; RoIs with an out-of-range
+// batch index are written by the extra grid row N (0 / -1).
+constexpr int kStKeys = 256;       // key = dh * 16 + dw (dh, dw <= 15); 0 empty; 255 large
+constexpr int kStLarge = 255;
+constexpr int kStMaxRB = 64;       // slot field of a record: 6 bits
+
+__host__ __device__ constexpr size_t st_fixed_bytes() { return 2 * kStKeys * 4 + 64 * 4 + 256; }
+__host__ __device__ constexpr size_t st_units(int rb, int phw) { return static_cast<size_t>(rb) * phw / 64 + kStKeys + 2; }
+__host__ __device__ constexpr size_t st_roi_bytes(int cg, int phw) {
+    return 16 + 2 * static_cast<size_t>(cg) * phw * 4 + static_cast<size_t>(phw) * 4;
+}
+
+template <int NT, int CG, bool HEAD, bool LIST>
+__global__ __launch_bounds__(NT) void roi_pool_fwd_staged_kernel(
+    const float* __restrict__ x, const float* __restrict__ rois, const int* __restrict__ list,
+    const int* __restrict__ cnt, int R, int C, int H, int W, int PH, int PW, float ss,
+    float* __restrict__ out, int32_t* __restrict__ argmax, int RB, HeadArgs hd) {
+    constexpr int NP = CG / 4;
+    extern __shared__ __attribute__((aligned(16))) float4 q4[];
+    const int PHW = PH * PW;
+    const int b = blockIdx.y;
+    const int c0 = blockIdx.x * CG;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int HW = H * W;
+    const int HWs = (HW + 15) & ~15;
+    const int split = gridDim.z, z = blockIdx.z;
+    // LDS carve (the tile at offset 0)
+    char* lp = reinterpret_cast<char*>(q4 + NP * HWs);
+    float* st_out = reinterpret_cast<float*>(lp);                       lp += static_cast<size_t>(RB) * CG * PHW * 4;
+    int32_t* st_am = reinterpret_cast<int32_t*>(lp);                    lp += static_cast<size_t>(RB) * CG * PHW * 4;
+    int4* s_geo = reinterpret_cast<int4*>(lp);                          lp += static_cast<size_t>(RB) * 16;
+    uint32_t* s_rec = reinterpret_cast<uint32_t*>(lp);                  lp += static_cast<size_t>(RB) * PHW * 4;
+    int2* s_unit = reinterpret_cast<int2*>(lp);                         lp += st_units(RB, PHW) * 8;
+    int* s_cnt = reinterpret_cast<int*>(lp);                            lp += kStKeys * 4;
+    int* s_off = reinterpret_cast<int*>(lp);                            lp += kStKeys * 4;
+    int* s_misc = reinterpret_cast<int*>(lp);                           // 64 ints
+    auto load_box = [&](int r, float (&bx)[5]) {
+        if (HEAD) {
+            head_box(rois, hd, r, bx);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 5; ++j) bx[j] = rois[static_cast<size_t>(r) * 5 + j];
+        }
+    };
+
+    // ---- 0. the image's RoIs [rbase, rbase + nr) (LIST: list[b][0, nr)), this workgroup's share
+    const int N = LIST ? gridDim.y : gridDim.y - 1;
+    if (!LIST && b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
+        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, 0, N, s_misc, 1)
+                             : roi_range_sorted<NT>(rois, R, 0, N, s_misc);
+        const int n_lo = rg.x, tot = n_lo + (R - rg.y);
+        const int lo = static_cast<int>(static_cast<int64_t>(tot) * z / split);
+        const int hi = static_cast<int>(static_cast<int64_t>(tot) * (z + 1) / split);
+        if (HEAD && hd.boxes && blockIdx.x == 0)
+            for (int t = lo + tid; t < hi; t += NT) {
+                const int r = t < n_lo ? t : rg.y + (t - n_lo);
+                float bx[5];
+                head_box(rois, hd, r, bx);
+#pragma unroll
+                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
+            }
+        for (int e = lo * CG * PHW + tid; e < hi * CG * PHW; e += NT) {
+            const int t = e / (CG * PHW);
+            const int rem = e - t * (CG * PHW);
+            const int r = t < n_lo ? t : rg.y + (t - n_lo);
+            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + rem;
+            out[o] = 0.0f;
+            argmax[o] = -1;
+        }
+        return;
+    }
+    int rbase = 0, nr;
+    if (LIST) {
+        nr = cnt[b];
+    } else {
+        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, b, b + 1, s_misc, 1)
+                             : roi_range_sorted<NT>(rois, R, b, b + 1, s_misc);
+        rbase = rg.x;
+        nr = rg.y - rg.x;
+    }
+    const int lo = static_cast<int>(static_cast<int64_t>(nr) * z / split);
+    const int hi = static_cast<int>(static_cast<int64_t>(nr) * (z + 1) / split);
+    if (lo >= hi) return;  // uniform
+    const int* lst = LIST ? list + static_cast<size_t>(b) * R : nullptr;
+    auto roi_of = [&](int t) { return LIST ? lst[t] : rbase + t; };
+
+    // ---- stage the CG planes
+    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+    for (int p = tid; p < HW; p += NT) {
+        float v[CG];
+#pragma unroll
+        for (int q = 0; q < CG; ++q) {
+            const float e = src[static_cast<size_t>(q) * HW + p];
+            v[q] = e != e ? -INFINITY : e;
+        }
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            q4[k * HWs + p] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    }
+
+    const int per4 = CG * PHW / 4;  // float4s of one RoI's output run
+    for (int r0 = lo; r0 < hi; r0 += RB) {
+        const int nb = min(RB, hi - r0);
+        const int nbin = nb * PHW;
+        // ---- 1a. geometry of the block's RoIs; clear the shape counts
+        for (int i = tid; i < kStKeys; i += NT) s_cnt[i] = 0;
+        if (tid == 0) s_misc[48] = 0;  // unit counter
+        for (int i = tid; i < nb; i += NT) {
+            const int r = roi_of(r0 + i);
+            float bx[5];
+            load_box(r, bx);
+            if (HEAD && hd.boxes && blockIdx.x == 0) {
+#pragma unroll
+                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
+            }
+            const RoiGeom gm = roi_geom(bx, ss, PH, PW);
+            s_geo[i] = make_int4(gm.sh, gm.sw, __float_as_int(gm.bh), __float_as_int(gm.bw));
+        }
+        __syncthreads();  // geometry + cleared counts; the previous block's flush is done with staging
+        // ---- 1b. shape key of every bin, rank among equal keys (ballots per wave)
+        constexpr int kMaxPer = (kStMaxRB * 64 + NT - 1) / NT;
+        int keyv[kMaxPer], offv[kMaxPer];
+        uint32_t recv[kMaxPer];
+#pragma unroll
+        for (int u = 0; u < kMaxPer; ++u) {
+            int t = tid + u * NT;
+            // opaque per block: the bin decode (t -> roi, ph, pw) is NOT hoisted out of
+            // the block loop, where 4 copies of it would live in VGPRs and spill
+            asm volatile("" : "+v"(t));
+            keyv[u] = -1;
+            if (u * NT >= nbin) continue;  // uniform
+            int key = -1;
+            uint32_t rec = 0;
+            if (t < nbin) {
+                const int i = t / PHW, k = t - (t / PHW) * PHW;
+                const int4 gq = s_geo[i];
+                RoiGeom gm;
+                gm.sh = gq.x;
+                gm.sw = gq.y;
+                gm.bh = __int_as_float(gq.z);
+                gm.bw = __int_as_float(gq.w);
+                const int ph = k / PW;
+                const int4 g = geom_bin(gm, H, W, ph, k - ph * PW);
+                const int dh = g.y - g.x, dw = g.w - g.z;
+                key = (dh <= 0 || dw <= 0) ? 0 : (dh > 15 || dw > 15) ? kStLarge : dh * 16 + dw;
+                rec = static_cast<uint32_t>(i) | (static_cast<uint32_t>(k) << 6) |
+                      (static_cast<uint32_t>(g.x) << 12) | (static_cast<uint32_t>(g.z) << 22);
+            }
+            int off = 0;
+            uint64_t todo = __ballot(key >= 0);
+            while (todo) {
+                const int l = __ffsll(static_cast<unsigned long long>(todo)) - 1;
+                const int lk = __builtin_amdgcn_readlane(key, l);
+                const uint64_t m = __ballot(key == lk);
+                int base = 0;
+                if (lane == l) base = atomicAdd(&s_cnt[lk], static_cast<int>(__popcll(m)));
+                base = __builtin_amdgcn_readlane(base, l);
+                if (key == lk) off = base + static_cast<int>(__popcll(m & lanemask_lt()));
+                todo &= ~m;
+            }
+            keyv[u] = key;
+            offv[u] = off;
+            recv[u] = rec;
+        }
+        __syncthreads();
+        // ---- 1c. (wave 0) keys in descending order -> record offsets and units
+        if (wid == 0) {
+            int c[4], uo[4], tot = 0, utot = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int key = kStKeys - 1 - (4 * lane + j);
+                c[j] = s_cnt[key];
+                uo[j] = (c[j] + 63) >> 6;
+                tot += c[j];
+                utot += uo[j];
+            }
+            int incl = tot, uincl = utot;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(incl, o, 64), uv = __shfl_up(uincl, o, 64);
+                if (lane >= o) {
+                    incl += v;
+                    uincl += uv;
+                }
+            }
+            int ro = incl - tot, uu = uincl - utot;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int key = kStKeys - 1 - (4 * lane + j);
+                s_off[key] = ro;
+                for (int q = 0; q < uo[j]; ++q)
+                    s_unit[uu + q] = make_int2(ro + 64 * q, (min(64, c[j] - 64 * q) << 8) | key);
+                ro += c[j];
+                uu += uo[j];
+            }
+            if (lane == 63) s_misc[49] = uincl;  // units of the block
+        }
+        __syncthreads();
+        // ---- 1d. records in sorted position
+#pragma unroll
+        for (int u = 0; u < kMaxPer; ++u)
+            if (keyv[u] >= 0) s_rec[s_off[keyv[u]] + offv[u]] = recv[u];
+        __syncthreads();
+        // ---- 2. units
+        const int nu = s_misc[49];
+        int ui = 0;
+        if (lane == 0) ui = atomicAdd(&s_misc[48], 1);
+        ui = __builtin_amdgcn_readfirstlane(ui);
+        while (ui < nu) {
+            int un = 0;
+            if (lane == 0) un = atomicAdd(&s_misc[48], 1);  // prefetch the next unit
+            const int2 unit = s_unit[ui];
+            const int key = __builtin_amdgcn_readfirstlane(unit.y & 255);
+            const int cu = __builtin_amdgcn_readfirstlane(unit.y >> 8);
+            const uint32_t rec = lane < cu ? s_rec[unit.x + lane] : 0u;
+            const int i = rec & 63, k = (rec >> 6) & 63;
+            const int hs = (rec >> 12) & 1023, wsx = rec >> 22;
+            float mv[CG];
+            int mi[CG];
+#pragma unroll
+            for (int c = 0; c < CG; ++c) {
+                mv[c] = key == 0 ? 0.0f : -FLT_MAX;
+                mi[c] = -1;
+            }
+            if (key == kStLarge) {  // per-lane windows
+                const int4 gq = s_geo[i];
+                RoiGeom gm;
+                gm.sh = gq.x;
+                gm.sw = gq.y;
+                gm.bh = __int_as_float(gq.z);
+                gm.bw = __int_as_float(gq.w);
+                const int ph = k / PW;
+                const int4 g = geom_bin(gm, H, W, ph, k - ph * PW);
+                for (int h = g.x; h < g.y; ++h)
+                    for (int w = g.z; w < g.w; w += 2) {
+                        const int a = h * W + w, bb = h * W + min(w + 1, g.w - 1);
+                        bs_pair<CG>(q4, HWs, a, bb, a, bb, mv, mi);
+                    }
+            } else if (key != 0) {
+                const int dh = key >> 4, dw = key & 15;
+                const int pix0 = hs * W + wsx;
+                switch (dw) {
+                    case 1: bs_scan_dw<CG, 1>(q4, HWs, W, pix0, dh, mv, mi); break;
+                    case 2: bs_scan_dw<CG, 2>(q4, HWs, W, pix0, dh, mv, mi); break;
+                    case 3: bs_scan_dw<CG, 3>(q4, HWs, W, pix0, dh, mv, mi); break;
+                    case 4: bs_scan_dw<CG, 4>(q4, HWs, W, pix0, dh, mv, mi); break;
+                    default:
+                        for (int ii = 0; ii < dh; ++ii) {
+                            const int p = pix0 + ii * W;
+                            for (int j = 0; j < dw; j += 2) {
+                                const int bb = p + min(j + 1, dw - 1);
+                                bs_pair<CG>(q4, HWs, p + j, bb, p + j, bb, mv, mi);
+                            }
+                        }
+                }
+            }
+            // a zero maximum keeps the sign of the first max pixel (max3 may return +0)
+            bool zero = false;
+#pragma unroll
+            for (int c = 0; c < CG; ++c) zero |= mv[c] == 0.0f && mi[c] >= 0;
+            if (__ballot(zero)) {
+#pragma unroll
+                for (int c = 0; c < CG; ++c)
+                    if (mv[c] == 0.0f && mi[c] >= 0)
+                        mv[c] = reinterpret_cast<const float*>(q4 + (c >> 2) * HWs + mi[c])[c & 3];
+            }
+            if (lane < cu) {
+                const int so = i * CG * PHW + k;
+#pragma unroll
+                for (int c = 0; c < CG; ++c) {
+                    st_out[so + c * PHW] = mv[c];
+                    st_am[so + c * PHW] = mi[c];
+                }
+            }
+            ui = __builtin_amdgcn_readfirstlane(un);
+        }
+        __syncthreads();
+        // ---- 3. the block's outputs: one contiguous run per RoI (16-B stores)
+        const float4* so4 = reinterpret_cast<const float4*>(st_out);
+        const int4* sa4 = reinterpret_cast<const int4*>(st_am);
+        for (int e = tid; e < nb * per4; e += NT) {
+            const int i = e / per4, q = e - (e / per4) * per4;
+            const size_t g4 = ((static_cast<size_t>(roi_of(r0 + i)) * C + c0) * PHW) / 4 + q;
+            reinterpret_cast<float4*>(out)[g4] = so4[e];
+            reinterpret_cast<int4*>(argmax)[g4] = sa4[e];
+        }
+        // (the next block's first barrier keeps its staging writes behind these reads)
+    }
+}
+
 // nets/heads.py:42-47 (fp32 divide, then multiply) + [idx, box] pack.
 __global__ __launch_bounds__(256) void roi_transform_kernel(const float* __restrict__ rois,
                                                             const float* __restrict__ inds,
@@ -1344,6 +1652,65 @@ BsPlan bs_plan(int C, int N, int H, int W, int PHW, int64_t R) {
     return pl;
 }
 
+// Launch plan of the block-sorted forward: CG = 8 if its tile leaves room
+// for a block of >= 16 RoIs, else 4 (the larger block), RB = RoIs per block
+// from the LDS left over, split = RoI shares per (image, channel group) so the
+// grid fills every CU once.
+struct StPlan {
+    int cg = 0, rb = 0, split = 1;
+    size_t lds = 0;
+};
+StPlan st_plan(int C, int N, int H, int W, int PHW) {
+    StPlan pl;
+    const size_t HW = static_cast<size_t>(H) * W;
+    if (N <= 0 || HW == 0 || PHW > 64 || H > 1023 || W > 1023) return pl;
+    const size_t HWs = (HW + 15) & ~static_cast<size_t>(15);
+    StPlan best;
+    for (int cg : {8, 4}) {  // (16 channels need > 128 VGPRs with the unit walk: spills)
+        if (C % cg != 0) continue;
+        if (path_cfg().roi_cg && cg != path_cfg().roi_cg) continue;  // A/B override
+        const size_t tile = static_cast<size_t>(cg / 4) * HWs * sizeof(float4);
+        const size_t fixed = st_fixed_bytes() + (kStKeys + 2) * 8 + 64;
+        if (tile + fixed >= kLdsPerCu) continue;
+        const size_t per = st_roi_bytes(cg, PHW) + (PHW * 8 + 63) / 64;
+        int rb = static_cast<int>((kLdsPerCu - tile - fixed) / per);
+        rb = rb > kStMaxRB ? kStMaxRB : rb;
+        if (rb < 4) continue;
+        StPlan p;
+        p.cg = cg;
+        p.rb = rb;
+        p.lds = tile + static_cast<size_t>(rb) * st_roi_bytes(cg, PHW) + st_units(rb, PHW) * 8 + st_fixed_bytes();
+        if (rb >= 16) {
+            best = p;
+            break;
+        }
+        if (p.rb > best.rb) best = p;
+    }
+    if (!best.cg) return pl;
+    const int64_t wgs = static_cast<int64_t>(C / best.cg) * N;
+    const int64_t target = device_cu_count();
+    int64_t sp = (target + wgs - 1) / wgs;
+    if (path_cfg().roi_split > 0) sp = path_cfg().roi_split;  // A/B override
+    best.split = static_cast<int>(sp < 1 ? 1 : (sp > 64 ? 64 : sp));
+    return best;
+}
+
+template <bool HEAD, bool LIST>
+int st_launch(const StPlan& pl, const float* x, const float* rois, const int* list, const int* cnt, int64_t R,
+              int N, int C, int H, int W, int PH, int PW, float ss, float* out, int32_t* argmax,
+              const HeadArgs& hd, hipStream_t st) {
+    const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(LIST ? N : N + 1),
+                    static_cast<unsigned>(pl.split));
+#define FRCNN_ST(CG)                                                                                      \
+    hipLaunchKernelGGL((roi_pool_fwd_staged_kernel<1024, CG, HEAD, LIST>), grid, dim3(1024), pl.lds, st, x, \
+                       rois, list, cnt, static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.rb, hd)
+    if (pl.cg == 8) FRCNN_ST(8);
+    else FRCNN_ST(4);
+#undef FRCNN_ST
+    FRCNN_LAUNCH_CHECK("roi_pool_fwd_staged_kernel");
+    return FRCNN_OK;
+}
+
 template <bool HEAD, bool LIST>
 int bs_launch(const BsPlan& pl, const FwdWs& w, const float* x, const float* rois, const float* boxes5,
               int64_t R, int N, int C, int H, int W, int PH, int PW, float ss, float* out, int32_t* argmax,
@@ -1453,6 +1820,29 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
     FRCNN_REQUIRE(x && rois && out && argmax, "frcnn_roi_pool_fwd: null pointer");
     hipStream_t st = as_stream(stream);
     const int path = path_cfg().roi_fwd;
+    const bool out_aligned = (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
+                             (reinterpret_cast<uintptr_t>(argmax) % 16 == 0);
+    const StPlan sp = (path == kPathStaged && out_aligned)
+                          ? st_plan(C, N, H, W, PH * PW)
+                          : StPlan{};
+    if (sp.cg) {
+        if (rois_sorted)
+            return st_launch<false, false>(sp, x, rois, nullptr, nullptr, R, N, C, H, W, PH, PW, spatial_scale,
+                                           out, argmax, HeadArgs{}, st);
+        FwdWs w = carve_fwd(workspace, R, N);
+        FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_fwd: workspace %zu < %zu",
+                      ws_bytes, w.bytes);
+        hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, rois, static_cast<int>(R), N,
+                           w.list, w.cnt);
+        FRCNN_LAUNCH_CHECK("roi_lists_kernel");
+        int rc = st_launch<false, true>(sp, x, rois, w.list, w.cnt, R, N, C, H, W, PH, PW, spatial_scale, out,
+                                        argmax, HeadArgs{}, st);
+        if (rc) return rc;
+        hipLaunchKernelGGL(roi_pool_invalid_fill_kernel, dim3(64), dim3(256), 0, st, w.list, w.cnt,
+                           static_cast<int>(R), N, static_cast<size_t>(C) * PH * PW, out, argmax);
+        FRCNN_LAUNCH_CHECK("roi_pool_invalid_fill_kernel");
+        return FRCNN_OK;
+    }
     const BsPlan bp = path == kPathSorted ? bs_plan(C, N, H, W, PH * PW, R) : BsPlan{};
     if (bp.cg) {
         FwdWs w = carve_fwd(workspace, R, N);
@@ -1518,6 +1908,32 @@ extern "C" int frcnn_roi_pool_fwd_head(const float* x, const float* rois, const 
     FRCNN_REQUIRE(rois && roi_inds && boxes, "frcnn_roi_pool_fwd_head: null pointer");
     const int path = path_cfg().roi_fwd;
     const bool aligned = reinterpret_cast<uintptr_t>(rois) % 16 == 0;
+    const bool out_aligned = (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
+                             (reinterpret_cast<uintptr_t>(argmax) % 16 == 0);
+    const StPlan sp = (C > 0 && aligned && out_aligned && path == kPathStaged)
+                          ? st_plan(C, N, H, W, PH * PW)
+                          : StPlan{};
+    if (sp.cg) {  // transform + pack inside the pool kernel, any RoI order
+        FRCNN_REQUIRE(x && out && argmax, "frcnn_roi_pool_fwd_head: null pointer");
+        const HeadArgs hd{roi_inds, img_h, img_w, static_cast<float>(H), static_cast<float>(W), boxes};
+        hipStream_t st = as_stream(stream);
+        if (rois_sorted)
+            return st_launch<true, false>(sp, x, rois, nullptr, nullptr, R, N, C, H, W, PH, PW, spatial_scale,
+                                          out, argmax, hd, st);
+        FwdWs w = carve_fwd(workspace, R, N);
+        FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_fwd_head: workspace %zu < %zu",
+                      ws_bytes, w.bytes);
+        hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, roi_inds, static_cast<int>(R), N,
+                           w.list, w.cnt, 1);
+        FRCNN_LAUNCH_CHECK("roi_lists_kernel");
+        int rc = st_launch<true, true>(sp, x, rois, w.list, w.cnt, R, N, C, H, W, PH, PW, spatial_scale, out,
+                                       argmax, hd, st);
+        if (rc) return rc;
+        hipLaunchKernelGGL(roi_pool_invalid_fill_kernel, dim3(64), dim3(256), 0, st, w.list, w.cnt,
+                           static_cast<int>(R), N, static_cast<size_t>(C) * PH * PW, out, argmax, rois, hd);
+        FRCNN_LAUNCH_CHECK("roi_pool_invalid_fill_kernel");
+        return FRCNN_OK;
+    }
     const BsPlan bp = (C > 0 && aligned && path == kPathSorted)
                           ? bs_plan(C, N, H, W, PH * PW, R)
                           : BsPlan{};
