@@ -491,7 +491,7 @@ def main():
                    "devices": min(world, ndev)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "roi_pool_bwd_pf_kernel" if train else "roi_pool_fwd_dense_kernel<head>",
+                     "kernel": "roi_pool_bwd_pf_kernel" if train else "roi_pool_fwd_wave_kernel<head>",
                      "kernel_us": dom_ms * 1e3, "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": None,
         "host_issue_us_per_step": t_issue / args.steps * 1e6,

@@ -40,8 +40,9 @@ int frcnn_device_cu_count(int* out);
 
 /* Kernel-path selection, process-global (tests and A/B tools; the default
  * "auto" is what every caller should use).  op / path:
- *   "roi_pool_fwd"   : "auto" | "sorted" (image tile in LDS, bins sorted by window shape)
- *                      | "dense" (image tile, a RoI's bins per wave) | "generic" (one workgroup per RoI)
+ *   "roi_pool_fwd"   : "auto" | "wave" (image tile in LDS, one wave per RoI; RoIs grouped by
+ *                      image) | "dense" (image tile, bins packed 64 per wave; any RoI order)
+ *                      | "generic" (one workgroup per RoI)
  *   "roi_pool_bwd"   : "auto" | "ring" (latency-hidden plane owner) | "plain"
  *   "propose"        : "auto" | "hybrid" | "lazy" (fused per image) | "wide" (chip-wide bitmask)
  *   "roi_pool_split" : "auto" | "1".."64" (RoI shares per image and channel group)

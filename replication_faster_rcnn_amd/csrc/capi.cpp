@@ -57,12 +57,10 @@ extern "C" int frcnn_set_path(const char* op, const char* path) {
     }
     auto is = [&](const char* a, const char* b) { return std::strcmp(a, b) == 0; };
     const bool aut = is(path, "auto");
-    if (is(op, "roi_pool_fwd") &&
-        (aut || is(path, "staged") || is(path, "sorted") || is(path, "dense") || is(path, "generic"))) {
+    if (is(op, "roi_pool_fwd") && (aut || is(path, "wave") || is(path, "dense") || is(path, "generic"))) {
         g_path.roi_fwd = aut ? kPathAuto : is(path, "generic") ? kPathGeneric
                                        : is(path, "dense")     ? kPathDense
-                                       : is(path, "staged")    ? kPathStaged
-                                                               : kPathSorted;
+                                                               : kPathWave;
     } else if (is(op, "roi_pool_bwd") && (aut || is(path, "ring") || is(path, "plain"))) {
         g_path.roi_bwd = is(path, "plain") ? kPathPlain : kPathAuto;
     } else if (is(op, "propose") &&
@@ -78,8 +76,6 @@ extern "C" int frcnn_set_path(const char* op, const char* path) {
             return FRCNN_EINVAL;
         }
         g_path.roi_split = static_cast<int>(v);
-    } else if (is(op, "roi_pool_probe")) {
-        g_path.roi_probe = std::atoi(path);
     } else if (is(op, "roi_pool_cg") && (aut || is(path, "4") || is(path, "8") || is(path, "16"))) {
         g_path.roi_cg = aut ? 0 : std::atoi(path);
     } else {

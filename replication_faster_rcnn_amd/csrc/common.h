@@ -18,8 +18,7 @@ void set_error(const char* fmt, ...);
 constexpr int kPathAuto = 0;
 constexpr int kPathGeneric = 1;  // roi_pool_fwd: one workgroup per RoI
 constexpr int kPathDense = 2;    // roi_pool_fwd: image tile, RoI bins packed per wave
-constexpr int kPathSorted = 3;   // roi_pool_fwd: image tile, bins sorted by window shape per image
-constexpr int kPathStaged = 4;   // roi_pool_fwd: image tile, bins sorted per RoI block, LDS-staged output
+constexpr int kPathWave = 3;     // roi_pool_fwd: image tile, one wave per RoI (RoIs grouped by image)
 constexpr int kPathPlain = 1;    // roi_pool_bwd: the unpipelined plane-owner kernel
 constexpr int kPathHybrid = 1;   // propose: fused per image + chip-wide first-chunk mask
 constexpr int kPathLazy = 2;     // propose: fused per image, lazy NMS from the first chunk on
@@ -30,7 +29,6 @@ struct PathCfg {
     int propose = kPathAuto;
     int roi_split = 0;  // RoI shares per (image, channel group); 0 = auto
     int roi_cg = 0;     // channels per RoIPool workgroup (4 / 8 / 16); 0 = auto
-    int roi_probe = 0;  // TEMPORARY timing probe: 1 = sorted forward without its output stores
 };
 const PathCfg& path_cfg();
 

@@ -242,7 +242,7 @@ constexpr int kDenseMisc = 64;
 __host__ __device__ constexpr size_t dense_fixed_bytes() { return 256 * 4 + kDenseMisc * 4; }
 __host__ __device__ constexpr size_t dense_item_bytes() { return 16 + 4 + 4 + 1; }
 
-template <int NT, int CG, int FIX, bool HEAD, bool LIST, int PROBE = 0>
+template <int NT, int CG, int FIX, bool HEAD, bool LIST>
 __global__ __launch_bounds__(NT) void roi_pool_fwd_dense_kernel(
     const float* __restrict__ x, const float* __restrict__ rois, const int* __restrict__ list,
     const int* __restrict__ cnt, int R, int C, int H, int W, int PH_, int PW_, float ss,
@@ -501,7 +501,7 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_dense_kernel(
                     for (int c = 0; c < CG; ++c) mv[c] = m2[c];
                 }
             }
-            if (live && (PROBE == 0 || mv[0] == 1234.5f)) {
+            if (live) {
                 const int r = s_rid[item];
                 const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + k;
 #pragma unroll
@@ -519,490 +519,43 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_dense_kernel(
     }
 }
 
-// ------------------------------------------------------ shape-sorted forward
-// The window of bin (ph, pw) is [hs, he) x [ws, we); on VOC-shaped RoIs the
-// mean window is ~8 pixels and a RoI's 49 windows differ by a row / column,
-// so a wave whose lanes are one RoI's bins runs every lane for the LARGEST
-// window (and per-lane loop control).  Here a prep kernel sorts every bin of
-// an image by its window shape (dh, dw) -- counting sort, one workgroup per
-// image -- and cuts each shape class into units of <= 64 bins.  The pool
-// kernel's waves take one unit at a time: the shape is wave-uniform, so the
-// walk is scalar-controlled, fully unrolled for dw <= 4 with the pixel offsets
-// as LDS immediates, and no lane ever scans past its own window.
-//   record (8 B per bin): { RoI index, k | hs << 10 | ws << 21 }
-//   unit   (8 B):         { first record, count << 12 | key },  key = dh*64 + dw
-// Units are balanced into `S` shares per image by a cost estimate (pairs per
-// window); one pool workgroup owns (image, CG channels, share).
-constexpr int kBsKeys = 4096;
-constexpr int kBsEmpty = 0;           // dh == 0 || dw == 0: out 0, argmax -1
-constexpr int kBsHuge = kBsKeys - 1;  // dh or dw > kBsMaxDim: per-lane windows
-constexpr int kBsMaxDim = 62;
-constexpr int kBsCap = 4096;          // RoI geometries per prep chunk (64 KB of LDS)
-constexpr int kBsMaxSplit = 64;
-
-struct BsWs {
-    int2* recs;    // [R * PHW]: image b's records at [rec_base(b), + its bins)
-    int2* units;   // [R * PHW + N]: image b's units at rec_base(b) + b
-    int* info;     // [N][2]: first unit, unit count
-    int* shares;   // [N][S + 1]: unit boundaries of the shares (relative)
-};
-
-__device__ __forceinline__ int bs_key(int4 g) {
-    const int dh = g.y - g.x, dw = g.w - g.z;
-    if (dh <= 0 || dw <= 0) return kBsEmpty;
-    if (dh > kBsMaxDim || dw > kBsMaxDim) return kBsHuge;
-    return dh * 64 + dw;
-}
-
-// Issue-cost estimate of one unit (VALU-bound: ~pairs of pixels x channels).
-__device__ __forceinline__ int bs_cost(int key) {
-    if (key == kBsEmpty) return 2;
-    if (key == kBsHuge) return 4096;
-    return (key >> 6) * (((key & 63) + 1) >> 1) * 2 + 6;
-}
-
-// Exclusive block scan of 3 ints per thread (NT threads); returns the prefix,
-// `tot` = the block totals.  `red` holds 3 * NT/64 ints.
-template <int NT>
-__device__ __forceinline__ int3 block_scan3(int3 v, int* red, int3& tot) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    int3 inc = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        const int a = __shfl_up(inc.x, o, 64), b = __shfl_up(inc.y, o, 64), c = __shfl_up(inc.z, o, 64);
-        if (lane >= o) {
-            inc.x += a;
-            inc.y += b;
-            inc.z += c;
-        }
-    }
-    if (lane == 63) {
-        red[3 * wid] = inc.x;
-        red[3 * wid + 1] = inc.y;
-        red[3 * wid + 2] = inc.z;
-    }
-    __syncthreads();
-    int3 pre = make_int3(inc.x - v.x, inc.y - v.y, inc.z - v.z);
-    tot = make_int3(0, 0, 0);
-    for (int w = 0; w < NT / 64; ++w) {
-        if (w < wid) {
-            pre.x += red[3 * w];
-            pre.y += red[3 * w + 1];
-            pre.z += red[3 * w + 2];
-        }
-        tot.x += red[3 * w];
-        tot.y += red[3 * w + 1];
-        tot.z += red[3 * w + 2];
-    }
-    __syncthreads();
-    return pre;
-}
-
-// One workgroup per image (blockIdx.x = b; when !LIST, block N writes the
-// outputs of RoIs with an out-of-range batch index).  HEAD: `rois` are [R,4]
-// image boxes + hd.inds, transformed here (nets/heads.py:42-47) and written to
-// hd.boxes.  LIST: RoIs in any order via roi_lists_kernel's lists.
-template <int NT, bool HEAD, bool LIST>
-__global__ __launch_bounds__(NT) void roi_binsort_kernel(const float* __restrict__ rois,
-                                                         const int* __restrict__ list,
-                                                         const int* __restrict__ cnt, int R, int N, int C,
-                                                         int H, int W, int PH, int PW, float ss, int S,
-                                                         BsWs ws, float* __restrict__ out,
-                                                         int32_t* __restrict__ argmax, HeadArgs hd) {
-    __shared__ int s_h[kBsKeys];
-    __shared__ int s_red[3 * (NT / 64)];
-    extern __shared__ __attribute__((aligned(16))) int4 s_geo[];  // kBsCap
-    const int b = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int PHW = PH * PW;
-    auto load_box = [&](int r, float (&bx)[5]) {
-        if (HEAD) {
-            head_box(rois, hd, r, bx);
-        } else {
-#pragma unroll
-            for (int j = 0; j < 5; ++j) bx[j] = rois[static_cast<size_t>(r) * 5 + j];
-        }
-    };
-    if (!LIST && b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
-        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, 0, N, s_red, 1)
-                             : roi_range_sorted<NT>(rois, R, 0, N, s_red);
-        const int n_lo = rg.x, tot = rg.x + (R - rg.y);
-        if (HEAD)
-            for (int t = tid; t < tot; t += NT) {
-                const int r = t < n_lo ? t : rg.y + (t - n_lo);
-                float bx[5];
-                head_box(rois, hd, r, bx);
-#pragma unroll
-                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
-            }
-        const int64_t per = static_cast<int64_t>(C) * PHW;
-        for (int64_t e = tid; e < tot * per; e += NT) {
-            const int t = static_cast<int>(e / per);
-            const int r = t < n_lo ? t : rg.y + (t - n_lo);
-            const size_t o = static_cast<size_t>(r) * per + (e - t * per);
-            out[o] = 0.0f;
-            argmax[o] = -1;
-        }
-        return;
-    }
-    int rbase = 0, nr;
-    int64_t first = 0;  // RoIs of the images before b
-    if (LIST) {
-        nr = cnt[b];
-        int acc = 0;
-        for (int i = tid; i < b; i += NT) acc += cnt[i];
-        int3 tot3;
-        block_scan3<NT>(make_int3(acc, 0, 0), s_red, tot3);
-        first = tot3.x;
-    } else {
-        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, b, b + 1, s_red, 1)
-                             : roi_range_sorted<NT>(rois, R, b, b + 1, s_red);
-        rbase = rg.x;
-        nr = rg.y - rg.x;
-        first = rbase;
-    }
-    const int rec_base = static_cast<int>(first * PHW);
-    const int ubase = rec_base + b;
-    auto roi_of = [&](int t) { return LIST ? list[static_cast<size_t>(b) * R + t] : rbase + t; };
-    for (int i = tid; i < kBsKeys; i += NT) s_h[i] = 0;
-
-    // pass 0: histogram of the window shapes (chunks of kBsCap RoI geometries)
-    auto chunk_geo = [&](int c0, int cn, bool write_boxes) {
-        __syncthreads();
-        for (int i = tid; i < cn; i += NT) {
-            const int r = roi_of(c0 + i);
-            float bx[5];
-            load_box(r, bx);
-            if (HEAD && write_boxes) {
-#pragma unroll
-                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
-            }
-            const RoiGeom gm = roi_geom(bx, ss, PH, PW);
-            s_geo[i] = make_int4(gm.sh, gm.sw, __float_as_int(gm.bh), __float_as_int(gm.bw));
-        }
-        __syncthreads();
-    };
-    auto bin_of = [&](int i, int k) {
-        const int4 gq = s_geo[i];
-        RoiGeom gm;
-        gm.sh = gq.x;
-        gm.sw = gq.y;
-        gm.bh = __int_as_float(gq.z);
-        gm.bw = __int_as_float(gq.w);
-        const int ph = k / PW;
-        return geom_bin(gm, H, W, ph, k - ph * PW);
-    };
-    for (int c0 = 0; c0 < nr; c0 += kBsCap) {
-        const int cn = min(kBsCap, nr - c0);
-        chunk_geo(c0, cn, true);
-        for (int t = tid; t < cn * PHW; t += NT) {
-            const int i = t / PHW;
-            atomicAdd(&s_h[bs_key(bin_of(i, t - i * PHW))], 1);
-        }
-    }
-    __syncthreads();
-
-    // scan: per key (records, units, cost); thread t owns keys 4t..4t+3
-    static_assert(kBsKeys == 4 * NT, "4 keys per thread");
-    int kc[4], ku[4], kcost[4];
-    int3 loc = make_int3(0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int key = 4 * tid + j;
-        kc[j] = s_h[key];
-        ku[j] = (kc[j] + 63) >> 6;
-        kcost[j] = bs_cost(key);
-        loc.x += kc[j];
-        loc.y += ku[j];
-        loc.z += ku[j] * kcost[j];
-    }
-    int3 tot;
-    int3 pre = block_scan3<NT>(loc, s_red, tot);
-    const int U = tot.y;
-    const double ctot = static_cast<double>(tot.z);
-    int* shares = ws.shares + static_cast<size_t>(b) * (S + 1);
-    if (U == 0)  // no RoI: every share empty (no key owns a boundary)
-        for (int z = tid; z <= S; z += NT) shares[z] = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int key = 4 * tid + j;
-        for (int q = 0; q < ku[j]; ++q)
-            ws.units[ubase + pre.y + q] =
-                make_int2(rec_base + pre.x + 64 * q, (min(64, kc[j] - 64 * q) << 12) | key);
-        // share z starts at the first unit whose cost midpoint reaches z/S of the total
-        if (ku[j] > 0)
-            for (int z = 1; z < S; ++z) {
-                const double T = ctot * z / S;
-                const double lo = pre.z, hi = pre.z + static_cast<double>(ku[j]) * kcost[j];
-                if (T >= lo && T < hi) {
-                    double q = ceil((T - lo) / kcost[j] - 0.5);
-                    q = q < 0 ? 0 : (q > ku[j] ? ku[j] : q);
-                    shares[z] = pre.y + static_cast<int>(q);
-                }
-            }
-        s_h[key] = pre.x;  // record cursor of the key (own slots only: no race)
-        pre.x += kc[j];
-        pre.y += ku[j];
-        pre.z += ku[j] * kcost[j];
-    }
-    if (tid == 0) {
-        shares[0] = 0;
-        shares[S] = U;
-        ws.info[2 * b] = ubase;
-        ws.info[2 * b + 1] = U;
-    }
-    // a share boundary no key owns (T == total exactly is impossible for z < S;
-    // all-zero cost cannot happen: every unit costs >= 2)
-
-    // pass 1: scatter the records
-    for (int c0 = 0; c0 < nr; c0 += kBsCap) {
-        const int cn = min(kBsCap, nr - c0);
-        chunk_geo(c0, cn, false);
-        for (int t = tid; t < cn * PHW; t += NT) {
-            const int i = t / PHW;
-            const int k = t - i * PHW;
-            const int4 g = bin_of(i, k);
-            const int pos = atomicAdd(&s_h[bs_key(g)], 1);
-            ws.recs[rec_base + pos] = make_int2(roi_of(c0 + i), k | (g.x << 10) | (g.z << 21));
-        }
-    }
-}
-
-// Strict-'>' first-max update of CG running (max, index) pairs with the pixel
-// pair (a, b) in row-major order: m' = max3(m, a, b); the index moves iff
-// m' > m, to a if a == m'.  pa / pb: the pixels' tile slots in plane 0.
-template <int CG>
-__device__ __forceinline__ void bs_pair(const float4* __restrict__ q4, int HWs, int sa, int sb, int ia,
-                                        int ib, float (&mv)[CG], int (&mi)[CG]) {
+// ------------------------------------------------- wave-per-RoI forward
+// The default forward for RoIs grouped by image.  One 1024-thread workgroup
+// owns CG channel planes of one image (staged once into LDS as CG/4 planes of
+// 4 channels, pixel-major, XOR-swizzled inside each 16-pixel group so that a
+// ds_read_b128 of bins a bin width apart does not collide) and a strided
+// share of that image's RoIs (items z, z+split, ...: RoI sizes are
+// uncorrelated with rank, so every share sees the image's size mix).  One
+// wave per RoI, lane = bin: each lane walks its window once and updates CG
+// (max, first index) pairs with torchvision's strict '>' -- the RoI geometry,
+// the window walk and the pixel address are shared by CG channels.  Waves pull
+// RoIs from an LDS counter (RoI sizes vary 100x); the RoI geometry of a chunk
+// of RoIs is computed once per workgroup into LDS.  Output: per channel, the
+// 49 lanes write one contiguous 196-B run.
+// HEAD: fused with the head's RoI transform (nets/heads.py:42-47): `rois` are
+// the [R,4] image boxes, hd.inds their image index; the [idx, box] rows are
+// formed in registers and (channel group 0) written to hd.boxes.
+// (Measured alternatives -- RoI bins packed 64 per wave, bins sorted by window
+// shape per image or per RoI block -- are slower: DESIGN.md §3.)
+template <int NT, int CG, bool HEAD>
+__global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
+    const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W, int PH, int PW,
+    float ss, float* __restrict__ out, int32_t* __restrict__ argmax, int geo_cap, HeadArgs hd) {
     constexpr int NP = CG / 4;
-    float4 va[NP], vb[NP];
-#pragma unroll
-    for (int q = 0; q < NP; ++q) {
-        va[q] = q4[q * HWs + sa];
-        vb[q] = q4[q * HWs + sb];
-    }
-#pragma unroll
-    for (int q = 0; q < NP; ++q) {
-        const float a4[4] = {va[q].x, va[q].y, va[q].z, va[q].w};
-        const float b4[4] = {vb[q].x, vb[q].y, vb[q].z, vb[q].w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int c = 4 * q + j;
-            const float m = max3_raw(mv[c], a4[j], b4[j]);
-            const int ip = a4[j] == m ? ia : ib;
-            mi[c] = m > mv[c] ? ip : mi[c];
-            mv[c] = m;
-        }
-    }
-    // one pair's 2*CG loaded values in flight at a time (CG = 16: 32 VGPRs); the
-    // other waves of the SIMD hide the LDS latency -- hoisting the next pair's
-    // loads spills at the 128-VGPR budget of a 1024-thread workgroup
-    __builtin_amdgcn_sched_barrier(0);
-}
-
-// Window walk for a wave-uniform shape: dh rows (runtime, uniform) of DW
-// pixels (compile time), row-major pairs; odd DW pairs across two rows.
-template <int CG, int DW>
-__device__ __forceinline__ void bs_scan_dw(const float4* __restrict__ q4, int HWs, int W, int pix0, int dh,
-                                           float (&mv)[CG], int (&mi)[CG]) {
-    if (DW % 2 == 0) {
-        for (int i = 0; i < dh; ++i) {
-            const int p = pix0 + i * W;
-#pragma unroll
-            for (int j = 0; j < DW; j += 2) bs_pair<CG>(q4, HWs, p + j, p + j + 1, p + j, p + j + 1, mv, mi);
-        }
-    } else {
-        int i = 0;
-        for (; i + 1 < dh; i += 2) {
-            const int p0 = pix0 + i * W, p1 = p0 + W;
-#pragma unroll
-            for (int t = 0; t < 2 * DW; t += 2) {
-                const int a = t < DW ? p0 + t : p1 + (t - DW);
-                const int b = t + 1 < DW ? p0 + t + 1 : p1 + (t + 1 - DW);
-                bs_pair<CG>(q4, HWs, a, b, a, b, mv, mi);
-            }
-        }
-        if (i < dh) {
-            const int p = pix0 + i * W;
-#pragma unroll
-            for (int j = 0; j < DW; j += 2) {
-                const int b = j + 1 < DW ? p + j + 1 : p + j;
-                bs_pair<CG>(q4, HWs, p + j, b, p + j, b, mv, mi);
-            }
-        }
-    }
-}
-
-template <int NT, int CG, int PROBE = 0>
-__global__ __launch_bounds__(NT) void roi_pool_fwd_sorted_kernel(
-    const float* __restrict__ x, const float* __restrict__ boxes5, BsWs ws, int S, int C, int H, int W,
-    int PH, int PW, float ss, float* __restrict__ out, int32_t* __restrict__ argmax) {
-    constexpr int NP = CG / 4;
-    extern __shared__ __attribute__((aligned(16))) float4 q4[];
+    extern __shared__ __attribute__((aligned(16))) float4 q4[];  // plane k at q4 + k * HWs; geometry after
+    __shared__ int s_red[2 * (NT / 64)];
     __shared__ int s_next;
-    const int b = blockIdx.y, z = blockIdx.z;
-    const int c0 = blockIdx.x * CG;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int* sh = ws.shares + static_cast<size_t>(b) * (S + 1);
-    const int u0 = sh[z], u1 = sh[z + 1];
-    if (u0 >= u1) return;  // uniform
-    const int2* units = ws.units + ws.info[2 * b] + u0;
-    const int nu = u1 - u0;
-    const int HW = H * W;
-    const int HWs = (HW + 15) & ~15;
-    const int PHW = PH * PW;
-
-    // stage the CG planes, NaN -> -inf (never selected by the strict '>' against
-    // the -FLT_MAX start; max3 then never sees a NaN)
-    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
-    for (int p = tid; p < HW; p += NT) {
-        float v[CG];
-#pragma unroll
-        for (int q = 0; q < CG; ++q) {
-            const float e = src[static_cast<size_t>(q) * HW + p];
-            v[q] = e != e ? -INFINITY : e;
-        }
-#pragma unroll
-        for (int k = 0; k < NP; ++k)
-            q4[k * HWs + p] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
-    }
-    if (tid == 0) s_next = 0;
-    __syncthreads();
-
-    int i = 0;
-    if (lane == 0) i = atomicAdd(&s_next, 1);
-    i = __builtin_amdgcn_readfirstlane(i);
-    while (i < nu) {
-        int in = 0;
-        if (lane == 0) in = atomicAdd(&s_next, 1);  // prefetch the next unit
-        const int2 un = units[i];
-        const int key = __builtin_amdgcn_readfirstlane(un.y & 4095);
-        const int cu = __builtin_amdgcn_readfirstlane(un.y >> 12);
-        const int2 rec = lane < cu ? ws.recs[un.x + lane] : make_int2(0, 0);
-        const int r = rec.x;
-        const int k = rec.y & 1023;
-        const int hs = (rec.y >> 10) & 2047, wsx = (rec.y >> 21) & 2047;
-        float mv[CG];
-        int mi[CG];
-#pragma unroll
-        for (int c = 0; c < CG; ++c) {
-            mv[c] = key == kBsEmpty ? 0.0f : -FLT_MAX;
-            mi[c] = -1;
-        }
-        if (key == kBsHuge) {  // per-lane windows (dh or dw > kBsMaxDim)
-            const RoiGeom gm = roi_geom(boxes5 + static_cast<size_t>(r) * 5, ss, PH, PW);
-            const int ph = k / PW;
-            const int4 g = geom_bin(gm, H, W, ph, k - ph * PW);
-            for (int h = g.x; h < g.y; ++h)
-                for (int w = g.z; w < g.w; w += 2) {
-                    const int a = h * W + w, bb = h * W + min(w + 1, g.w - 1);
-                    bs_pair<CG>(q4, HWs, a, bb, a, bb, mv, mi);
-                }
-        } else if (key != kBsEmpty) {
-            const int dh = key >> 6, dw = key & 63;
-            const int pix0 = hs * W + wsx;
-            switch (dw) {
-                case 1: bs_scan_dw<CG, 1>(q4, HWs, W, pix0, dh, mv, mi); break;
-                case 2: bs_scan_dw<CG, 2>(q4, HWs, W, pix0, dh, mv, mi); break;
-                case 3: bs_scan_dw<CG, 3>(q4, HWs, W, pix0, dh, mv, mi); break;
-                case 4: bs_scan_dw<CG, 4>(q4, HWs, W, pix0, dh, mv, mi); break;
-                default:
-                    for (int ii = 0; ii < dh; ++ii) {
-                        const int p = pix0 + ii * W;
-                        for (int j = 0; j < dw; j += 2) {
-                            const int bb = p + min(j + 1, dw - 1);
-                            bs_pair<CG>(q4, HWs, p + j, bb, p + j, bb, mv, mi);
-                        }
-                    }
-            }
-        }
-        // a zero maximum keeps the sign of the first max pixel (max3 may return +0)
-        bool zero = false;
-#pragma unroll
-        for (int c = 0; c < CG; ++c) zero |= mv[c] == 0.0f && mi[c] >= 0;
-        if (__ballot(zero)) {
-#pragma unroll
-            for (int c = 0; c < CG; ++c)
-                if (mv[c] == 0.0f && mi[c] >= 0)
-                    mv[c] = reinterpret_cast<const float*>(q4 + (c >> 2) * HWs + mi[c])[c & 3];
-        }
-        if (lane < cu && (PROBE == 0 || mv[0] == 1234.5f)) {
-            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + k;
-#pragma unroll
-            for (int c = 0; c < CG; ++c) {
-                out[o + static_cast<size_t>(c) * PHW] = mv[c];
-                argmax[o + static_cast<size_t>(c) * PHW] = mi[c];
-            }
-        }
-        i = __builtin_amdgcn_readfirstlane(in);
-    }
-}
-
-// ------------------------------------------------- block-sorted forward
-// The default forward.  A workgroup owns CG channel planes of one image
-// (staged once into LDS, NaN -> -inf) and a contiguous share of that image's
-// RoIs, taken RB RoIs (a "block") at a time:
-//   1. the block's RB*PH*PW bins are counting-sorted by window shape
-//      (dh, dw) -- wave ballots rank equal shapes, one LDS atomic per
-//      (wave, shape) -- and cut into units of <= 64 bins of ONE shape,
-//      largest shapes first;
-//   2. waves pull units: the window walk is wave-uniform (scalar loop
-//      control, dw <= 4 fully unrolled with LDS immediates, no lane runs past
-//      its own window -- a RoI-per-wave mapping runs every lane for the RoI's
-//      largest window, 1.5x the pixels on VOC-shaped RoIs, and leaves 15 of 64
-//      lanes idle) and write their (max, argmax) pairs into an LDS staging
-//      image of the block's outputs;
-//   3. the block's outputs leave as contiguous 16-B stores: RoI r's channels
-//      [c0, c0+CG) x PH*PW are one run of out / argmax.
-// Window sizes > 15 fall back to per-lane walks; RoIs with an out-of-range
-// batch index are written by the extra grid row N (0 / -1).
-constexpr int kStKeys = 256;       // key = dh * 16 + dw (dh, dw <= 15); 0 empty; 255 large
-constexpr int kStLarge = 255;
-constexpr int kStMaxRB = 64;       // slot field of a record: 6 bits
-
-__host__ __device__ constexpr size_t st_fixed_bytes() { return 2 * kStKeys * 4 + 64 * 4 + 256; }
-__host__ __device__ constexpr size_t st_units(int rb, int phw) { return static_cast<size_t>(rb) * phw / 64 + kStKeys + 2; }
-__host__ __device__ constexpr size_t st_roi_bytes(int cg, int phw) {
-    return 16 + 2 * static_cast<size_t>(cg) * phw * 4 + static_cast<size_t>(phw) * 4;
-}
-
-template <int NT, int CG, bool HEAD, bool LIST>
-__global__ __launch_bounds__(NT) void roi_pool_fwd_staged_kernel(
-    const float* __restrict__ x, const float* __restrict__ rois, const int* __restrict__ list,
-    const int* __restrict__ cnt, int R, int C, int H, int W, int PH, int PW, float ss,
-    float* __restrict__ out, int32_t* __restrict__ argmax, int RB, HeadArgs hd) {
-    constexpr int NP = CG / 4;
-    extern __shared__ __attribute__((aligned(16))) float4 q4[];
-    const int PHW = PH * PW;
     const int b = blockIdx.y;
     const int c0 = blockIdx.x * CG;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
     const int HW = H * W;
     const int HWs = (HW + 15) & ~15;
+    const int PHW = PH * PW;
     const int split = gridDim.z, z = blockIdx.z;
-    // LDS carve (the tile at offset 0)
-    char* lp = reinterpret_cast<char*>(q4 + NP * HWs);
-    float* st_out = reinterpret_cast<float*>(lp);                       lp += static_cast<size_t>(RB) * CG * PHW * 4;
-    int32_t* st_am = reinterpret_cast<int32_t*>(lp);                    lp += static_cast<size_t>(RB) * CG * PHW * 4;
-    int4* s_geo = reinterpret_cast<int4*>(lp);                          lp += static_cast<size_t>(RB) * 16;
-    uint32_t* s_rec = reinterpret_cast<uint32_t*>(lp);                  lp += static_cast<size_t>(RB) * PHW * 4;
-    int2* s_unit = reinterpret_cast<int2*>(lp);                         lp += st_units(RB, PHW) * 8;
-    int* s_cnt = reinterpret_cast<int*>(lp);                            lp += kStKeys * 4;
-    int* s_off = reinterpret_cast<int*>(lp);                            lp += kStKeys * 4;
-    int* s_misc = reinterpret_cast<int*>(lp);                           // 64 ints
-    auto load_box = [&](int r, float (&bx)[5]) {
-        if (HEAD) {
-            head_box(rois, hd, r, bx);
-        } else {
-#pragma unroll
-            for (int j = 0; j < 5; ++j) bx[j] = rois[static_cast<size_t>(r) * 5 + j];
-        }
-    };
-
-    // ---- 0. the image's RoIs [rbase, rbase + nr) (LIST: list[b][0, nr)), this workgroup's share
-    const int N = LIST ? gridDim.y : gridDim.y - 1;
-    if (!LIST && b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
-        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, 0, N, s_misc, 1)
-                             : roi_range_sorted<NT>(rois, R, 0, N, s_misc);
+    const int N = gridDim.y - 1;
+    if (b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
+        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, 0, N, s_red, 1)
+                             : roi_range_sorted<NT>(rois, R, 0, N, s_red);
         const int n_lo = rg.x, tot = n_lo + (R - rg.y);
         const int lo = static_cast<int>(static_cast<int64_t>(tot) * z / split);
         const int hi = static_cast<int>(static_cast<int64_t>(tot) * (z + 1) / split);
@@ -1024,221 +577,99 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_staged_kernel(
         }
         return;
     }
-    int rbase = 0, nr;
-    if (LIST) {
-        nr = cnt[b];
-    } else {
-        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, b, b + 1, s_misc, 1)
-                             : roi_range_sorted<NT>(rois, R, b, b + 1, s_misc);
-        rbase = rg.x;
-        nr = rg.y - rg.x;
-    }
-    const int lo = static_cast<int>(static_cast<int64_t>(nr) * z / split);
-    const int hi = static_cast<int>(static_cast<int64_t>(nr) * (z + 1) / split);
-    if (lo >= hi) return;  // uniform
-    const int* lst = LIST ? list + static_cast<size_t>(b) * R : nullptr;
-    auto roi_of = [&](int t) { return LIST ? lst[t] : rbase + t; };
-
-    // ---- stage the CG planes
+    const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, b, b + 1, s_red, 1)
+                         : roi_range_sorted<NT>(rois, R, b, b + 1, s_red);
+    const int rbase = rg.x, nr = rg.y - rg.x;
+    if (z >= nr) return;
+    const int nmine = (nr - z + split - 1) / split;  // items z, z+split, ...
     const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
     for (int p = tid; p < HW; p += NT) {
         float v[CG];
 #pragma unroll
-        for (int q = 0; q < CG; ++q) {
-            const float e = src[static_cast<size_t>(q) * HW + p];
-            v[q] = e != e ? -INFINITY : e;
-        }
+        for (int q = 0; q < CG; ++q) v[q] = src[static_cast<size_t>(q) * HW + p];
+        const int s = p ^ ((p >> 4) & 15);
 #pragma unroll
         for (int k = 0; k < NP; ++k)
-            q4[k * HWs + p] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+            q4[k * HWs + s] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
     }
-
-    const int per4 = CG * PHW / 4;  // float4s of one RoI's output run
-    for (int r0 = lo; r0 < hi; r0 += RB) {
-        const int nb = min(RB, hi - r0);
-        const int nbin = nb * PHW;
-        // ---- 1a. geometry of the block's RoIs; clear the shape counts
-        for (int i = tid; i < kStKeys; i += NT) s_cnt[i] = 0;
-        if (tid == 0) s_misc[48] = 0;  // unit counter
-        for (int i = tid; i < nb; i += NT) {
-            const int r = roi_of(r0 + i);
+    int4* s_geo = reinterpret_cast<int4*>(q4 + NP * HWs);
+    const int ph = lane / PW, pw = lane - (lane / PW) * PW;
+    const bool act = lane < PHW;
+    for (int k0 = 0; k0 < nmine; k0 += geo_cap) {
+        const int cn = min(geo_cap, nmine - k0);
+        for (int i = tid; i < cn; i += NT) {
+            const int r = rbase + z + (k0 + i) * split;
             float bx[5];
-            load_box(r, bx);
-            if (HEAD && hd.boxes && blockIdx.x == 0) {
+            if (HEAD) {
+                head_box(rois, hd, r, bx);
+                if (hd.boxes && blockIdx.x == 0) {
 #pragma unroll
-                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
+                    for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 5; ++j) bx[j] = rois[static_cast<size_t>(r) * 5 + j];
             }
             const RoiGeom gm = roi_geom(bx, ss, PH, PW);
             s_geo[i] = make_int4(gm.sh, gm.sw, __float_as_int(gm.bh), __float_as_int(gm.bw));
         }
-        __syncthreads();  // geometry + cleared counts; the previous block's flush is done with staging
-        // ---- 1b. shape key of every bin, rank among equal keys (ballots per wave)
-        constexpr int kMaxPer = (kStMaxRB * 64 + NT - 1) / NT;
-        int keyv[kMaxPer], offv[kMaxPer];
-        uint32_t recv[kMaxPer];
-#pragma unroll
-        for (int u = 0; u < kMaxPer; ++u) {
-            int t = tid + u * NT;
-            // opaque per block: the bin decode (t -> roi, ph, pw) is NOT hoisted out of
-            // the block loop, where 4 copies of it would live in VGPRs and spill
-            asm volatile("" : "+v"(t));
-            keyv[u] = -1;
-            if (u * NT >= nbin) continue;  // uniform
-            int key = -1;
-            uint32_t rec = 0;
-            if (t < nbin) {
-                const int i = t / PHW, k = t - (t / PHW) * PHW;
-                const int4 gq = s_geo[i];
-                RoiGeom gm;
-                gm.sh = gq.x;
-                gm.sw = gq.y;
-                gm.bh = __int_as_float(gq.z);
-                gm.bw = __int_as_float(gq.w);
-                const int ph = k / PW;
-                const int4 g = geom_bin(gm, H, W, ph, k - ph * PW);
-                const int dh = g.y - g.x, dw = g.w - g.z;
-                key = (dh <= 0 || dw <= 0) ? 0 : (dh > 15 || dw > 15) ? kStLarge : dh * 16 + dw;
-                rec = static_cast<uint32_t>(i) | (static_cast<uint32_t>(k) << 6) |
-                      (static_cast<uint32_t>(g.x) << 12) | (static_cast<uint32_t>(g.z) << 22);
-            }
-            int off = 0;
-            uint64_t todo = __ballot(key >= 0);
-            while (todo) {
-                const int l = __ffsll(static_cast<unsigned long long>(todo)) - 1;
-                const int lk = __builtin_amdgcn_readlane(key, l);
-                const uint64_t m = __ballot(key == lk);
-                int base = 0;
-                if (lane == l) base = atomicAdd(&s_cnt[lk], static_cast<int>(__popcll(m)));
-                base = __builtin_amdgcn_readlane(base, l);
-                if (key == lk) off = base + static_cast<int>(__popcll(m & lanemask_lt()));
-                todo &= ~m;
-            }
-            keyv[u] = key;
-            offv[u] = off;
-            recv[u] = rec;
-        }
+        if (tid == 0) s_next = 0;
         __syncthreads();
-        // ---- 1c. (wave 0) keys in descending order -> record offsets and units
-        if (wid == 0) {
-            int c[4], uo[4], tot = 0, utot = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int key = kStKeys - 1 - (4 * lane + j);
-                c[j] = s_cnt[key];
-                uo[j] = (c[j] + 63) >> 6;
-                tot += c[j];
-                utot += uo[j];
-            }
-            int incl = tot, uincl = utot;
-            for (int o = 1; o < 64; o <<= 1) {
-                const int v = __shfl_up(incl, o, 64), uv = __shfl_up(uincl, o, 64);
-                if (lane >= o) {
-                    incl += v;
-                    uincl += uv;
-                }
-            }
-            int ro = incl - tot, uu = uincl - utot;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int key = kStKeys - 1 - (4 * lane + j);
-                s_off[key] = ro;
-                for (int q = 0; q < uo[j]; ++q)
-                    s_unit[uu + q] = make_int2(ro + 64 * q, (min(64, c[j] - 64 * q) << 8) | key);
-                ro += c[j];
-                uu += uo[j];
-            }
-            if (lane == 63) s_misc[49] = uincl;  // units of the block
-        }
-        __syncthreads();
-        // ---- 1d. records in sorted position
-#pragma unroll
-        for (int u = 0; u < kMaxPer; ++u)
-            if (keyv[u] >= 0) s_rec[s_off[keyv[u]] + offv[u]] = recv[u];
-        __syncthreads();
-        // ---- 2. units
-        const int nu = s_misc[49];
-        int ui = 0;
-        if (lane == 0) ui = atomicAdd(&s_misc[48], 1);
-        ui = __builtin_amdgcn_readfirstlane(ui);
-        while (ui < nu) {
-            int un = 0;
-            if (lane == 0) un = atomicAdd(&s_misc[48], 1);  // prefetch the next unit
-            const int2 unit = s_unit[ui];
-            const int key = __builtin_amdgcn_readfirstlane(unit.y & 255);
-            const int cu = __builtin_amdgcn_readfirstlane(unit.y >> 8);
-            const uint32_t rec = lane < cu ? s_rec[unit.x + lane] : 0u;
-            const int i = rec & 63, k = (rec >> 6) & 63;
-            const int hs = (rec >> 12) & 1023, wsx = rec >> 22;
+        int k = 0;
+        if (lane == 0) k = atomicAdd(&s_next, 1);
+        k = __builtin_amdgcn_readfirstlane(k);
+        while (k < cn) {
+            int kn = 0;
+            if (lane == 0) kn = atomicAdd(&s_next, 1);  // prefetch the next item
+            const int r = rbase + z + (k0 + k) * split;
+            const int4 gq = s_geo[k];
+            RoiGeom gm;
+            gm.sh = gq.x;
+            gm.sw = gq.y;
+            gm.bh = __int_as_float(gq.z);
+            gm.bw = __int_as_float(gq.w);
+            int4 g = geom_bin(gm, H, W, ph, pw);
+            if (!act) g = make_int4(0, 0, 0, 0);
+            const bool empty = g.y <= g.x || g.w <= g.z;
             float mv[CG];
             int mi[CG];
 #pragma unroll
             for (int c = 0; c < CG; ++c) {
-                mv[c] = key == 0 ? 0.0f : -FLT_MAX;
+                mv[c] = empty ? 0.0f : -FLT_MAX;
                 mi[c] = -1;
             }
-            if (key == kStLarge) {  // per-lane windows
-                const int4 gq = s_geo[i];
-                RoiGeom gm;
-                gm.sh = gq.x;
-                gm.sw = gq.y;
-                gm.bh = __int_as_float(gq.z);
-                gm.bw = __int_as_float(gq.w);
-                const int ph = k / PW;
-                const int4 g = geom_bin(gm, H, W, ph, k - ph * PW);
-                for (int h = g.x; h < g.y; ++h)
-                    for (int w = g.z; w < g.w; w += 2) {
-                        const int a = h * W + w, bb = h * W + min(w + 1, g.w - 1);
-                        bs_pair<CG>(q4, HWs, a, bb, a, bb, mv, mi);
-                    }
-            } else if (key != 0) {
-                const int dh = key >> 4, dw = key & 15;
-                const int pix0 = hs * W + wsx;
-                switch (dw) {
-                    case 1: bs_scan_dw<CG, 1>(q4, HWs, W, pix0, dh, mv, mi); break;
-                    case 2: bs_scan_dw<CG, 2>(q4, HWs, W, pix0, dh, mv, mi); break;
-                    case 3: bs_scan_dw<CG, 3>(q4, HWs, W, pix0, dh, mv, mi); break;
-                    case 4: bs_scan_dw<CG, 4>(q4, HWs, W, pix0, dh, mv, mi); break;
-                    default:
-                        for (int ii = 0; ii < dh; ++ii) {
-                            const int p = pix0 + ii * W;
-                            for (int j = 0; j < dw; j += 2) {
-                                const int bb = p + min(j + 1, dw - 1);
-                                bs_pair<CG>(q4, HWs, p + j, bb, p + j, bb, mv, mi);
+            for (int h = g.x; h < g.y; ++h) {
+                const int rb = h * W;
+                for (int w = g.z; w < g.w; ++w) {
+                    const int ii = rb + w;
+                    const int s = ii ^ ((ii >> 4) & 15);
+                    float4 v[NP];
+#pragma unroll
+                    for (int q = 0; q < NP; ++q) v[q] = q4[q * HWs + s];
+#pragma unroll
+                    for (int q = 0; q < NP; ++q) {
+                        const float vv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            if (vv[j] > mv[4 * q + j]) {  // torchvision's strict '>'
+                                mv[4 * q + j] = vv[j];
+                                mi[4 * q + j] = ii;
                             }
                         }
+                    }
                 }
             }
-            // a zero maximum keeps the sign of the first max pixel (max3 may return +0)
-            bool zero = false;
-#pragma unroll
-            for (int c = 0; c < CG; ++c) zero |= mv[c] == 0.0f && mi[c] >= 0;
-            if (__ballot(zero)) {
-#pragma unroll
-                for (int c = 0; c < CG; ++c)
-                    if (mv[c] == 0.0f && mi[c] >= 0)
-                        mv[c] = reinterpret_cast<const float*>(q4 + (c >> 2) * HWs + mi[c])[c & 3];
-            }
-            if (lane < cu) {
-                const int so = i * CG * PHW + k;
+            if (act) {
+                const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
 #pragma unroll
                 for (int c = 0; c < CG; ++c) {
-                    st_out[so + c * PHW] = mv[c];
-                    st_am[so + c * PHW] = mi[c];
+                    out[o + static_cast<size_t>(c) * PHW] = mv[c];
+                    argmax[o + static_cast<size_t>(c) * PHW] = mi[c];
                 }
             }
-            ui = __builtin_amdgcn_readfirstlane(un);
+            k = __builtin_amdgcn_readfirstlane(kn);
         }
-        __syncthreads();
-        // ---- 3. the block's outputs: one contiguous run per RoI (16-B stores)
-        const float4* so4 = reinterpret_cast<const float4*>(st_out);
-        const int4* sa4 = reinterpret_cast<const int4*>(st_am);
-        for (int e = tid; e < nb * per4; e += NT) {
-            const int i = e / per4, q = e - (e / per4) * per4;
-            const size_t g4 = ((static_cast<size_t>(roi_of(r0 + i)) * C + c0) * PHW) / 4 + q;
-            reinterpret_cast<float4*>(out)[g4] = so4[e];
-            reinterpret_cast<int4*>(argmax)[g4] = sa4[e];
-        }
-        // (the next block's first barrier keeps its staging writes behind these reads)
+        __syncthreads();  // the chunk's geometry and s_next are reused
     }
 }
 
@@ -1601,140 +1032,66 @@ namespace {
 struct FwdWs {
     int* list;
     int* cnt;
-    BsWs bs;
     size_t bytes;
 };
-// Sized for PH*PW <= 64 (the shape-sorted path's records); the workspace-size
-// query does not know the output size.
 FwdWs carve_fwd(void* ws, int64_t R, int N) {
     Carver c(ws);
     FwdWs w{};
     w.list = c.take<int>(static_cast<size_t>(N + 1) * R);
     w.cnt = c.take<int>(N + 1);
-    w.bs.recs = c.take<int2>(static_cast<size_t>(R) * 64);
-    w.bs.units = c.take<int2>(static_cast<size_t>(R) * 64 + N);
-    w.bs.info = c.take<int>(static_cast<size_t>(2) * N);
-    w.bs.shares = c.take<int>(static_cast<size_t>(N) * (kBsMaxSplit + 1));
     w.bytes = c.used();
     return w;
 }
 
-// Launch plan of the shape-sorted forward: CG = 16 channel planes when they
-// fit the CU's LDS, else 8, else 4; split = cost-balanced unit shares per
-// (image, channel group), sized so the grid fills every resident slot once.
-struct BsPlan {
-    int cg = 0, split = 1;
+// Launch plan of the wave-per-RoI forward: CG = 16 channel planes when they
+// fit the CU's LDS (one workgroup per CU), else 8 (two per CU when they fit),
+// else 4.  Each workgroup gets the LDS left over for its RoI-geometry chunk;
+// split = RoI shares per (image, channel group), sized so the grid fills every
+// resident slot once.
+struct PxPlan {
+    int cg = 0, geo_cap = 0, split = 1;
     size_t lds = 0;
 };
-BsPlan bs_plan(int C, int N, int H, int W, int PHW, int64_t R) {
-    BsPlan pl;
+PxPlan px_plan(int C, int N, int H, int W, int PHW) {
+    PxPlan pl;
     const size_t HW = static_cast<size_t>(H) * W;
-    if (N <= 0 || HW == 0 || PHW > 64 || H > 2047 || W > 2047 || R * 64 >= (int64_t(1) << 31) - N)
-        return pl;
+    if (N <= 0 || HW == 0 || PHW > 64 || H > 65535 || W > 65535) return pl;
+    constexpr size_t kReserve = 1024;  // static LDS + allocation rounding
+    constexpr size_t kMinGeo = 64 * sizeof(int4);
     const size_t HWs = (HW + 15) & ~static_cast<size_t>(15);
-    constexpr size_t kReserve = 256;  // static LDS + allocation rounding
     for (int cg : {16, 8, 4}) {
         if (C % cg != 0) continue;
         if (path_cfg().roi_cg && cg != path_cfg().roi_cg) continue;  // A/B override
         const size_t tile = static_cast<size_t>(cg / 4) * HWs * sizeof(float4);
-        if (tile + kReserve > kLdsPerCu) continue;
-        int per_cu = static_cast<int>(kLdsPerCu / (tile + kReserve));
-        per_cu = per_cu > 2 ? 2 : per_cu;  // 1024-thread workgroups: <= 2 per CU
+        int per_cu = 0;
+        if (2 * (tile + kMinGeo + kReserve) <= kLdsPerCu) per_cu = 2;
+        else if (tile + kMinGeo + kReserve <= kLdsPerCu) per_cu = 1;
+        if (!per_cu) continue;
+        const size_t geo = (kLdsPerCu / per_cu - kReserve - tile) / sizeof(int4);
+        pl.geo_cap = static_cast<int>(geo > 512 ? 512 : geo);
         pl.cg = cg;
-        pl.lds = tile;
+        pl.lds = tile + static_cast<size_t>(pl.geo_cap) * sizeof(int4);
         const int64_t wgs = static_cast<int64_t>(C / cg) * N;
-        const int64_t target = static_cast<int64_t>(device_cu_count()) * per_cu;
-        int64_t sp = (target + wgs - 1) / wgs;
+        int64_t sp = (static_cast<int64_t>(device_cu_count()) * per_cu + wgs - 1) / wgs;
         if (path_cfg().roi_split > 0) sp = path_cfg().roi_split;  // A/B override
-        pl.split = static_cast<int>(sp < 1 ? 1 : (sp > kBsMaxSplit ? kBsMaxSplit : sp));
+        pl.split = static_cast<int>(sp < 1 ? 1 : (sp > 64 ? 64 : sp));
         return pl;
     }
     return pl;
 }
 
-// Launch plan of the block-sorted forward: CG = 8 if its tile leaves room
-// for a block of >= 16 RoIs, else 4 (the larger block), RB = RoIs per block
-// from the LDS left over, split = RoI shares per (image, channel group) so the
-// grid fills every CU once.
-struct StPlan {
-    int cg = 0, rb = 0, split = 1;
-    size_t lds = 0;
-};
-StPlan st_plan(int C, int N, int H, int W, int PHW) {
-    StPlan pl;
-    const size_t HW = static_cast<size_t>(H) * W;
-    if (N <= 0 || HW == 0 || PHW > 64 || H > 1023 || W > 1023) return pl;
-    const size_t HWs = (HW + 15) & ~static_cast<size_t>(15);
-    StPlan best;
-    for (int cg : {8, 4}) {  // (16 channels need > 128 VGPRs with the unit walk: spills)
-        if (C % cg != 0) continue;
-        if (path_cfg().roi_cg && cg != path_cfg().roi_cg) continue;  // A/B override
-        const size_t tile = static_cast<size_t>(cg / 4) * HWs * sizeof(float4);
-        const size_t fixed = st_fixed_bytes() + (kStKeys + 2) * 8 + 64;
-        if (tile + fixed >= kLdsPerCu) continue;
-        const size_t per = st_roi_bytes(cg, PHW) + (PHW * 8 + 63) / 64;
-        int rb = static_cast<int>((kLdsPerCu - tile - fixed) / per);
-        rb = rb > kStMaxRB ? kStMaxRB : rb;
-        if (rb < 4) continue;
-        StPlan p;
-        p.cg = cg;
-        p.rb = rb;
-        p.lds = tile + static_cast<size_t>(rb) * st_roi_bytes(cg, PHW) + st_units(rb, PHW) * 8 + st_fixed_bytes();
-        if (rb >= 16) {
-            best = p;
-            break;
-        }
-        if (p.rb > best.rb) best = p;
-    }
-    if (!best.cg) return pl;
-    const int64_t wgs = static_cast<int64_t>(C / best.cg) * N;
-    const int64_t target = device_cu_count();
-    int64_t sp = (target + wgs - 1) / wgs;
-    if (path_cfg().roi_split > 0) sp = path_cfg().roi_split;  // A/B override
-    best.split = static_cast<int>(sp < 1 ? 1 : (sp > 64 ? 64 : sp));
-    return best;
-}
-
-template <bool HEAD, bool LIST>
-int st_launch(const StPlan& pl, const float* x, const float* rois, const int* list, const int* cnt, int64_t R,
-              int N, int C, int H, int W, int PH, int PW, float ss, float* out, int32_t* argmax,
-              const HeadArgs& hd, hipStream_t st) {
-    const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(LIST ? N : N + 1),
-                    static_cast<unsigned>(pl.split));
-#define FRCNN_ST(CG)                                                                                      \
-    hipLaunchKernelGGL((roi_pool_fwd_staged_kernel<1024, CG, HEAD, LIST>), grid, dim3(1024), pl.lds, st, x, \
-                       rois, list, cnt, static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.rb, hd)
-    if (pl.cg == 8) FRCNN_ST(8);
-    else FRCNN_ST(4);
-#undef FRCNN_ST
-    FRCNN_LAUNCH_CHECK("roi_pool_fwd_staged_kernel");
-    return FRCNN_OK;
-}
-
-template <bool HEAD, bool LIST>
-int bs_launch(const BsPlan& pl, const FwdWs& w, const float* x, const float* rois, const float* boxes5,
-              int64_t R, int N, int C, int H, int W, int PH, int PW, float ss, float* out, int32_t* argmax,
-              const HeadArgs& hd, hipStream_t st) {
-    hipLaunchKernelGGL((roi_binsort_kernel<1024, HEAD, LIST>), dim3(LIST ? N : N + 1), dim3(1024),
-                       kBsCap * sizeof(int4), st, rois, w.list, w.cnt, static_cast<int>(R), N, C, H, W, PH,
-                       PW, ss, pl.split, w.bs, out, argmax, hd);
-    FRCNN_LAUNCH_CHECK("roi_binsort_kernel");
-    const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(N), static_cast<unsigned>(pl.split));
-#define FRCNN_BS(CG, PR)                                                                                    \
-    hipLaunchKernelGGL((roi_pool_fwd_sorted_kernel<1024, CG, PR>), grid, dim3(1024), pl.lds, st, x, boxes5, \
-                       w.bs, pl.split, C, H, W, PH, PW, ss, out, argmax)
-    if (path_cfg().roi_probe == 1) {
-        if (pl.cg == 16) FRCNN_BS(16, 1);
-        else if (pl.cg == 8) FRCNN_BS(8, 1);
-        else FRCNN_BS(4, 1);
-    } else if (path_cfg().roi_probe == 2) {  // prep only
-    } else {
-        if (pl.cg == 16) FRCNN_BS(16, 0);
-        else if (pl.cg == 8) FRCNN_BS(8, 0);
-        else FRCNN_BS(4, 0);
-    }
-#undef FRCNN_BS
-    FRCNN_LAUNCH_CHECK("roi_pool_fwd_sorted_kernel");
+template <bool HEAD>
+int px_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
+              int PH, int PW, float ss, float* out, int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
+    const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(N + 1), static_cast<unsigned>(pl.split));
+#define FRCNN_PX(CG)                                                                                    \
+    hipLaunchKernelGGL((roi_pool_fwd_wave_kernel<1024, CG, HEAD>), grid, dim3(1024), pl.lds, st, x, rois, \
+                       static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd)
+    if (pl.cg == 16) FRCNN_PX(16);
+    else if (pl.cg == 8) FRCNN_PX(8);
+    else FRCNN_PX(4);
+#undef FRCNN_PX
+    FRCNN_LAUNCH_CHECK("roi_pool_fwd_wave_kernel");
     return FRCNN_OK;
 }
 
@@ -1787,10 +1144,7 @@ int dense_launch(const DensePlan& pl, const float* x, const float* rois, const i
     hipLaunchKernelGGL((roi_pool_fwd_dense_kernel<1024, CG, FX, HEAD, LIST>), grid, dim3(1024), pl.lds, st, \
                        x, rois, list, cnt, static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.cap,  \
                        hd)
-    if (path_cfg().roi_probe == 1 && pl.cg == 16 && fix7)
-        hipLaunchKernelGGL((roi_pool_fwd_dense_kernel<1024, 16, 7, HEAD, LIST, 1>), grid, dim3(1024), pl.lds, st,
-                           x, rois, list, cnt, static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.cap, hd);
-    else if (pl.cg == 16) {
+    if (pl.cg == 16) {
         if (fix7) FRCNN_DENSE(16, 7); else FRCNN_DENSE(16, 0);
     } else if (pl.cg == 8) {
         if (fix7) FRCNN_DENSE(8, 7); else FRCNN_DENSE(8, 0);
@@ -1820,48 +1174,10 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
     FRCNN_REQUIRE(x && rois && out && argmax, "frcnn_roi_pool_fwd: null pointer");
     hipStream_t st = as_stream(stream);
     const int path = path_cfg().roi_fwd;
-    const bool out_aligned = (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
-                             (reinterpret_cast<uintptr_t>(argmax) % 16 == 0);
-    const StPlan sp = (path == kPathStaged && out_aligned)
-                          ? st_plan(C, N, H, W, PH * PW)
-                          : StPlan{};
-    if (sp.cg) {
-        if (rois_sorted)
-            return st_launch<false, false>(sp, x, rois, nullptr, nullptr, R, N, C, H, W, PH, PW, spatial_scale,
-                                           out, argmax, HeadArgs{}, st);
-        FwdWs w = carve_fwd(workspace, R, N);
-        FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_fwd: workspace %zu < %zu",
-                      ws_bytes, w.bytes);
-        hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, rois, static_cast<int>(R), N,
-                           w.list, w.cnt);
-        FRCNN_LAUNCH_CHECK("roi_lists_kernel");
-        int rc = st_launch<false, true>(sp, x, rois, w.list, w.cnt, R, N, C, H, W, PH, PW, spatial_scale, out,
-                                        argmax, HeadArgs{}, st);
-        if (rc) return rc;
-        hipLaunchKernelGGL(roi_pool_invalid_fill_kernel, dim3(64), dim3(256), 0, st, w.list, w.cnt,
-                           static_cast<int>(R), N, static_cast<size_t>(C) * PH * PW, out, argmax);
-        FRCNN_LAUNCH_CHECK("roi_pool_invalid_fill_kernel");
-        return FRCNN_OK;
-    }
-    const BsPlan bp = path == kPathSorted ? bs_plan(C, N, H, W, PH * PW, R) : BsPlan{};
-    if (bp.cg) {
-        FwdWs w = carve_fwd(workspace, R, N);
-        FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_fwd: workspace %zu < %zu",
-                      ws_bytes, w.bytes);
-        if (rois_sorted)
-            return bs_launch<false, false>(bp, w, x, rois, rois, R, N, C, H, W, PH, PW, spatial_scale, out,
-                                           argmax, HeadArgs{}, st);
-        hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, rois, static_cast<int>(R), N,
-                           w.list, w.cnt);
-        FRCNN_LAUNCH_CHECK("roi_lists_kernel");
-        int rc = bs_launch<false, true>(bp, w, x, rois, rois, R, N, C, H, W, PH, PW, spatial_scale, out,
-                                        argmax, HeadArgs{}, st);
-        if (rc) return rc;
-        hipLaunchKernelGGL(roi_pool_invalid_fill_kernel, dim3(64), dim3(256), 0, st, w.list, w.cnt,
-                           static_cast<int>(R), N, static_cast<size_t>(C) * PH * PW, out, argmax);
-        FRCNN_LAUNCH_CHECK("roi_pool_invalid_fill_kernel");
-        return FRCNN_OK;
-    }
+    const PxPlan xp = (rois_sorted && (path == kPathAuto || path == kPathWave)) ? px_plan(C, N, H, W, PH * PW)
+                                                                              : PxPlan{};
+    if (xp.cg)
+        return px_launch<false>(xp, x, rois, R, N, C, H, W, PH, PW, spatial_scale, out, argmax, HeadArgs{}, st);
     const DensePlan pl = path == kPathGeneric ? DensePlan{} : dense_plan(C, N, H, W, PH * PW);
     if (pl.cg && rois_sorted)
         return dense_launch<false, false>(pl, x, rois, nullptr, nullptr, R, N, C, H, W, PH, PW,
@@ -1908,57 +1224,16 @@ extern "C" int frcnn_roi_pool_fwd_head(const float* x, const float* rois, const 
     FRCNN_REQUIRE(rois && roi_inds && boxes, "frcnn_roi_pool_fwd_head: null pointer");
     const int path = path_cfg().roi_fwd;
     const bool aligned = reinterpret_cast<uintptr_t>(rois) % 16 == 0;
-    const bool out_aligned = (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
-                             (reinterpret_cast<uintptr_t>(argmax) % 16 == 0);
-    const StPlan sp = (C > 0 && aligned && out_aligned && path == kPathStaged)
-                          ? st_plan(C, N, H, W, PH * PW)
-                          : StPlan{};
-    if (sp.cg) {  // transform + pack inside the pool kernel, any RoI order
+    const PxPlan xp = (rois_sorted && C > 0 && aligned && (path == kPathAuto || path == kPathWave))
+                          ? px_plan(C, N, H, W, PH * PW)
+                          : PxPlan{};
+    if (xp.cg) {  // transform + pack inside the pool kernel
         FRCNN_REQUIRE(x && out && argmax, "frcnn_roi_pool_fwd_head: null pointer");
         const HeadArgs hd{roi_inds, img_h, img_w, static_cast<float>(H), static_cast<float>(W), boxes};
-        hipStream_t st = as_stream(stream);
-        if (rois_sorted)
-            return st_launch<true, false>(sp, x, rois, nullptr, nullptr, R, N, C, H, W, PH, PW, spatial_scale,
-                                          out, argmax, hd, st);
-        FwdWs w = carve_fwd(workspace, R, N);
-        FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_fwd_head: workspace %zu < %zu",
-                      ws_bytes, w.bytes);
-        hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, roi_inds, static_cast<int>(R), N,
-                           w.list, w.cnt, 1);
-        FRCNN_LAUNCH_CHECK("roi_lists_kernel");
-        int rc = st_launch<true, true>(sp, x, rois, w.list, w.cnt, R, N, C, H, W, PH, PW, spatial_scale, out,
-                                       argmax, hd, st);
-        if (rc) return rc;
-        hipLaunchKernelGGL(roi_pool_invalid_fill_kernel, dim3(64), dim3(256), 0, st, w.list, w.cnt,
-                           static_cast<int>(R), N, static_cast<size_t>(C) * PH * PW, out, argmax, rois, hd);
-        FRCNN_LAUNCH_CHECK("roi_pool_invalid_fill_kernel");
-        return FRCNN_OK;
+        return px_launch<true>(xp, x, rois, R, N, C, H, W, PH, PW, spatial_scale, out, argmax, hd,
+                               as_stream(stream));
     }
-    const BsPlan bp = (C > 0 && aligned && path == kPathSorted)
-                          ? bs_plan(C, N, H, W, PH * PW, R)
-                          : BsPlan{};
-    if (bp.cg) {  // transform + pack inside the prep kernel, any RoI order
-        FRCNN_REQUIRE(x && out && argmax, "frcnn_roi_pool_fwd_head: null pointer");
-        FwdWs w = carve_fwd(workspace, R, N);
-        FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_fwd_head: workspace %zu < %zu",
-                      ws_bytes, w.bytes);
-        const HeadArgs hd{roi_inds, img_h, img_w, static_cast<float>(H), static_cast<float>(W), boxes};
-        hipStream_t st = as_stream(stream);
-        if (rois_sorted)
-            return bs_launch<true, false>(bp, w, x, rois, boxes, R, N, C, H, W, PH, PW, spatial_scale, out,
-                                          argmax, hd, st);
-        hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, roi_inds, static_cast<int>(R), N,
-                           w.list, w.cnt, 1);
-        FRCNN_LAUNCH_CHECK("roi_lists_kernel");
-        int rc = bs_launch<true, true>(bp, w, x, rois, boxes, R, N, C, H, W, PH, PW, spatial_scale, out,
-                                       argmax, hd, st);
-        if (rc) return rc;
-        hipLaunchKernelGGL(roi_pool_invalid_fill_kernel, dim3(64), dim3(256), 0, st, w.list, w.cnt,
-                           static_cast<int>(R), N, static_cast<size_t>(C) * PH * PW, out, argmax, rois, hd);
-        FRCNN_LAUNCH_CHECK("roi_pool_invalid_fill_kernel");
-        return FRCNN_OK;
-    }
-    const DensePlan pl = (rois_sorted && C > 0 && path != kPathGeneric && path != kPathSorted)
+    const DensePlan pl = (rois_sorted && C > 0 && path != kPathGeneric)
                              ? dense_plan(C, N, H, W, PH * PW)
                              : DensePlan{};
     if (!pl.cg || reinterpret_cast<uintptr_t>(rois) % 16 != 0) {

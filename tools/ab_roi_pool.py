@@ -1,8 +1,8 @@
 """A/B timing of the RoIPool forward paths on one device, interleaved rounds.
 
-    python tools/ab_roi_pool.py [--config cfg2] [--variants sorted,sorted:8,dense@3,sorted/u,generic]
+    python tools/ab_roi_pool.py [--config cfg2] [--variants blocks,blocks:4,dense@3,dense/u,generic]
 
-A variant is `path[:cg][@split][/u]`: path = sorted | dense | generic
+A variant is `path[:cg][@split][/u]`: path = blocks | dense | generic
 (frcnn_set_path("roi_pool_fwd", path)), cg = channels per workgroup
 ("roi_pool_cg"), split = RoI / unit shares per image ("roi_pool_split"), /u =
 RoIs passed as unsorted (per-image lists first).
@@ -27,7 +27,7 @@ from replication_faster_rcnn_amd import anchors as A  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="cfg2")
-    ap.add_argument("--variants", default="sorted,dense")
+    ap.add_argument("--variants", default="blocks,dense")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
@@ -50,10 +50,8 @@ def main():
     for rnd in range(a.rounds):
         for vs in variants:
             v, uns = (vs[:-2], True) if vs.endswith("/u") else (vs, False)
-            v, _, probe = v.partition("!")
             v, _, sp = v.partition("@")
             v, _, cg = v.partition(":")
-            _lib.set_path("roi_pool_probe", probe or "0")
             _lib.set_path("roi_pool_split", sp or "auto")
             _lib.set_path("roi_pool_cg", cg or "auto")
             _lib.set_path("roi_pool_fwd", v)
@@ -61,7 +59,7 @@ def main():
             out, am = ops._roi_pool_fwd(x, boxes, 7, 7, 1.0, srt)
             if ref is None:
                 ref = (out.clone(), am.clone())
-            elif rnd == 0 and not probe:
+            elif rnd == 0:
                 assert torch.equal(out, ref[0]) and torch.equal(am, ref[1]), f"variant {vs} differs"
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -70,7 +68,6 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             times[vs].append(e0.elapsed_time(e1) / a.iters * 1e3)
-    _lib.set_path("roi_pool_probe", "0")
     for op in ("roi_pool_split", "roi_pool_cg", "roi_pool_fwd"):
         _lib.set_path(op, "auto")
     res = {v: {"us_median": float(np.median(t)), "us_min": float(np.min(t)),
