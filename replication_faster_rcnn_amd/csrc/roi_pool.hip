@@ -519,11 +519,21 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_dense_kernel(
     }
 }
 
+// Tile layout of the wave-per-RoI forward: 16-pixel groups, the group's NP
+// 4-channel planes back to back (pixel p of plane q at float4
+// (g*NP + q)*16 + s, g = p >> 4), the slot s = (p ^ g) & 15 XOR-swizzled so
+// that a ds_read_b128 of bins a bin width apart does not collide, and the
+// planes of one pixel 256 B apart -- LDS immediate offsets.
+template <int NP>
+__device__ __forceinline__ const float4* tile_px(const float4* q4, int p) {
+    const int g = p >> 4;
+    return q4 + g * (NP * 16) + ((p ^ g) & 15);
+}
+
 // ------------------------------------------------- wave-per-RoI forward
 // The default forward for RoIs grouped by image.  One 1024-thread workgroup
-// owns CG channel planes of one image (staged once into LDS as CG/4 planes of
-// 4 channels, pixel-major, XOR-swizzled inside each 16-pixel group so that a
-// ds_read_b128 of bins a bin width apart does not collide) and a strided
+// owns CG channel planes of one image (staged once into LDS, tile_px layout)
+// and a strided
 // share of that image's RoIs (items z, z+split, ...: RoI sizes are
 // uncorrelated with rank, so every share sees the image's size mix).  One
 // wave per RoI, lane = bin: each lane walks its window once and updates CG
@@ -586,11 +596,14 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
     for (int p = tid; p < HW; p += NT) {
         float v[CG];
 #pragma unroll
-        for (int q = 0; q < CG; ++q) v[q] = src[static_cast<size_t>(q) * HW + p];
-        const int s = p ^ ((p >> 4) & 15);
+        for (int q = 0; q < CG; ++q) {
+            const float e = src[static_cast<size_t>(q) * HW + p];
+            v[q] = e;
+        }
+        const float4* pp = tile_px<NP>(q4, p);
 #pragma unroll
         for (int k = 0; k < NP; ++k)
-            q4[k * HWs + s] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+            const_cast<float4*>(pp)[16 * k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
     }
     int4* s_geo = reinterpret_cast<int4*>(q4 + NP * HWs);
     const int ph = lane / PW, pw = lane - (lane / PW) * PW;
@@ -642,10 +655,13 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
                 const int rb = h * W;
                 for (int w = g.z; w < g.w; ++w) {
                     const int ii = rb + w;
-                    const int s = ii ^ ((ii >> 4) & 15);
+                    const float4* pp = tile_px<NP>(q4, ii);
                     float4 v[NP];
 #pragma unroll
-                    for (int q = 0; q < NP; ++q) v[q] = q4[q * HWs + s];
+                    for (int q = 0; q < NP; ++q) v[q] = pp[16 * q];
+                    // all NP reads in flight before the first compare (else the compiler
+                    // waits on each read in turn: NP LDS round trips per pixel)
+                    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                     for (int q = 0; q < NP; ++q) {
                         const float vv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
