@@ -12,6 +12,7 @@ rc=$?; tail -2 "$OUT/pytest.log"; [ $rc -ne 0 ] && exit $rc
 for c in cfg2 cfg4 cfg5; do
   timeout -k 10 200 python -u tools/ab_roi_pool.py --config $c --variants "$V" > "$OUT/ab_$c.log" 2>&1 || exit $?
 done
+timeout -k 10 200 python -u tools/ab_roi_pool_bwd.py > "$OUT/ab_bwd.log" 2>&1 || exit $?
 if [ "${3:-}" = pmc ]; then
   bash tools/pmc_roi_pool.sh "$OUT/pmc" "${V%%,*}" cfg2 > "$OUT/pmc.log" 2>&1 || exit $?
 fi
