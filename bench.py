@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--dist-backend", default="auto", choices=("auto", "nccl", "gloo"),
                     help="auto: nccl (RCCL over xGMI) when every rank has a GPU of its own, "
                          "gloo (host copies) when ranks share one")
+    ap.add_argument("--roi-cg", default="auto",
+                    help="channels per RoIPool forward workgroup (frcnn_set_path roi_pool_cg): auto | 4 | 8 | 16")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-baseline sample (rank 0, N=1 only); 0 disables")
     ap.add_argument("--cpu-images", type=int, default=10, help="minimum timed CPU images (median)")
@@ -281,58 +283,71 @@ def gather(rois, idx, cnt, n_total, backend):
 
 def inference_step_fn(args, c, sc, de, x, base, world, n_total, backend, ev):
     """cfg1-4: propose -> (all-gather of detections) -> RoI transform + pack +
-    RoIPool forward (nets/rpn.py:102-138, nets/heads.py:42-48)."""
+    RoIPool forward (nets/rpn.py:102-138, nets/heads.py:42-48).  Every buffer
+    and event is allocated once, outside the timed steps: proposal outputs per
+    proposal stream (reused once the pool that read them has finished), one set
+    of pooled outputs on the pool stream."""
     from replication_faster_rcnn_amd import ops
     N, dev = sc.size(0), sc.device
     post = c["post_nms"]
+    C = x.size(1)
     inds = torch.arange(N, device=dev, dtype=torch.float32).repeat_interleave(post)
     s_props, s_pool = make_streams(args)
+    nps = len(s_props)
+    prop_out = [(torch.empty((N, post, 4), dtype=torch.float32, device=dev),
+                 torch.empty((N, post), dtype=torch.int32, device=dev),
+                 torch.empty((N,), dtype=torch.int32, device=dev)) for _ in range(nps)]
+    pool_out = (torch.empty((N * post, C, 7, 7), dtype=torch.float32, device=dev),
+                torch.empty((N * post, C, 7, 7), dtype=torch.int32, device=dev),
+                torch.empty((N * post, 5), dtype=torch.float32, device=dev))
+    ready = [torch.cuda.Event() for _ in range(nps)]
+    done = [None] * nps          # the pool that last read prop_out[j]
+    done_ev = [torch.cuda.Event() for _ in range(nps)]
     k_step = [0]
     if args.host_io:  # reference-style host tensors: inputs H2D, rois + pooled D2H per step
         h_in = [t.cpu().pin_memory() for t in (sc, de, x)]
         d_in = [[torch.empty_like(t) for t in (sc, de, x)] for _ in s_props]
         h_rois = torch.empty((N, post, 4), dtype=torch.float32).pin_memory()
-        h_pool = torch.empty((N * post, x.size(1), 7, 7), dtype=torch.float32).pin_memory()
-        done = [None] * len(s_props)
+        h_pool = torch.empty((N * post, C, 7, 7), dtype=torch.float32).pin_memory()
     gathered = {}
 
     def step(timed):
-        j = k_step[0] % len(s_props)
+        j = k_step[0] % nps
         s_prop = s_props[j]
         k_step[0] += 1
+        rois, idx, cnt = prop_out[j]
         with torch.cuda.stream(s_prop):
+            if done[j] is not None:
+                s_prop.wait_event(done[j])  # the pool that read prop_out[j] (and d_in[j]) last time
             sc_, de_, x_ = sc, de, x
             if args.host_io:
-                if done[j] is not None:
-                    s_prop.wait_event(done[j])  # the pool that read d_in[j] last time
                 for d, h in zip(d_in[j], h_in):
                     d.copy_(h, non_blocking=True)
                 sc_, de_, x_ = d_in[j]
-            rois, idx, cnt = ops.propose(sc_, de_, img_w=c["img_w"], img_h=c["img_h"],
-                                         pre_nms=c["pre_nms"], post_nms=post, anchor_base=base,
-                                         feat_h=c["feat_h"], feat_w=c["feat_w"])
+            ops.propose(sc_, de_, img_w=c["img_w"], img_h=c["img_h"], pre_nms=c["pre_nms"],
+                        post_nms=post, anchor_base=base, feat_h=c["feat_h"], feat_w=c["feat_w"],
+                        out=prop_out[j])
             if world > 1:  # the only collective: detections of all ranks
                 gathered["last"] = gather(rois, idx, cnt, n_total, backend)
             if args.host_io:
                 h_rois.copy_(rois, non_blocking=True)
-            ready = torch.cuda.Event()
-            ready.record(s_prop)
+            ready[j].record(s_prop)
         with torch.cuda.stream(s_pool):
-            s_pool.wait_event(ready)
-            rois.record_stream(s_pool)  # allocated on s_prop, read on s_pool
+            s_pool.wait_event(ready[j])
             if timed:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0, e1 = ev["pairs"][ev["i"]]
+                ev["i"] += 1
                 e0.record(s_pool)
             # ResnetHead's transform + pack + roi_pool (nets/heads.py:42-48): one launch
-            pooled, am, boxes = ops.roi_pool_head(x_, rois.view(-1, 4), inds, 7, c["img_h"], c["img_w"],
-                                                  rois_sorted=True)
+            ops.roi_pool_head(x_, rois.view(-1, 4), inds, 7, c["img_h"], c["img_w"],
+                              rois_sorted=True, out=pool_out)
             if timed:
                 e1.record(s_pool)
                 ev["fwd"].append((e0, e1))
             if args.host_io:
-                h_pool.copy_(pooled, non_blocking=True)
-                done[j] = torch.cuda.Event()
-                done[j].record(s_pool)
+                h_pool.copy_(pool_out[0], non_blocking=True)
+            done_ev[j].record(s_pool)
+            done[j] = done_ev[j]
         return cnt
     step.gathered = gathered
     return step
@@ -400,7 +415,9 @@ def main():
     maybe_launch(args)
     world, rank, dev_index, backend, ndev = setup_dist(args)
     dev = torch.device("cuda", dev_index)
+    from replication_faster_rcnn_amd import _lib
     from replication_faster_rcnn_amd import anchors as A
+    _lib.set_path("roi_pool_cg", args.roi_cg)
     from replication_faster_rcnn_amd import dist as fdist
     from replication_faster_rcnn_amd import synth
     cfg = resolve_config(args, world)
@@ -420,7 +437,9 @@ def main():
     c, sc, de, x = make_inputs(cfg, mine, dev)
     N = sc.size(0)
     base = A.generate_anchor_base_device(anchor_scales=c["scales"])
-    ev = {"fwd": [], "bwd": []}
+    ev = {"fwd": [], "bwd": [], "i": 0,  # timing events allocated before the timed steps
+          "pairs": [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    for _ in range(args.steps)]}
     if train:
         step = train_step_fn(args, c, sc, de, x, base, mine.start, ev)
     else:
@@ -484,7 +503,7 @@ def main():
         "config": {"workload": workload, "global_batch": n_total,
                    "parallelism": f"dp{world} (per-image sharding)", "streams": args.streams,
                    "prop_streams": args.prop_streams if (args.streams == 2 and not train) else 1,
-                   "host_io": bool(args.host_io),
+                   "host_io": bool(args.host_io), "roi_cg": args.roi_cg,
                    "collective": (None if world == 1 else
                                   ("RCCL all_gather_into_tensor" if backend == "nccl"
                                    else "gloo all_gather_into_tensor (ranks share a GPU)")),

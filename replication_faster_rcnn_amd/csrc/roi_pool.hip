@@ -906,7 +906,10 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_pf_kernel(
     const int* __restrict__ list, const int* __restrict__ cnt,
     int R, int C, int HW, int PHW, int PW, int CPW, float* __restrict__ grad_in) {
     extern __shared__ __attribute__((aligned(16))) float planes[];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    // wave-uniform in an SGPR: the per-RoI grad / argmax bases are then scalar,
+    // and each lane's load is base (SGPR) + its bin offset (VGPR, fixed)
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int b = blockIdx.y;
     const int c = blockIdx.x * CPW + wid;
     if (c >= C) return;  // whole wave; no workgroup barrier below
@@ -940,10 +943,11 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_pf_kernel(
         for (int d = 0; d < D; ++d) {
             const int n = lst[d < nr ? d : nr - 1];
             const size_t base = (static_cast<size_t>(n) * C + c) * PHW;
-            am_r[d] = argmax[base + kl];
-            g_r[d] = grad[base + kl];
-            cd_r[d] = code[static_cast<size_t>(n) * PHW + kl];
-            cm_r[d] = cmask[static_cast<size_t>(n) * PHW + kl];
+            const size_t nb = static_cast<size_t>(n) * PHW;
+            am_r[d] = (argmax + base)[kl];
+            g_r[d] = (grad + base)[kl];
+            cd_r[d] = (code + nb)[kl];
+            cm_r[d] = (cmask + nb)[kl];
             // keep the loop's issue order (slot by slot): the waitcnt pass then
             // merges identical queues at the loop header instead of draining
             asm volatile("" ::: "memory");
@@ -979,10 +983,11 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_pf_kernel(
                 {  // refill this slot with RoI t + D before applying RoI t
                     const int n = nx[d];
                     const size_t base = (static_cast<size_t>(n) * C + c) * PHW;
-                    am_r[d] = argmax[base + kl];
-                    g_r[d] = grad[base + kl];
-                    cd_r[d] = code[static_cast<size_t>(n) * PHW + kl];
-                    cm_r[d] = cmask[static_cast<size_t>(n) * PHW + kl];
+                    const size_t nb = static_cast<size_t>(n) * PHW;
+                    am_r[d] = (argmax + base)[kl];
+                    g_r[d] = (grad + base)[kl];
+                    cd_r[d] = (code + nb)[kl];
+                    cm_r[d] = (cmask + nb)[kl];
                 }
                 // depth = rank of this bin among the RoI's bins with the same
                 // argmax pixel (those windows all contain the pixel, so they

@@ -104,13 +104,21 @@ class _RoIPoolFunction(torch.autograd.Function):
         return gi, None, None, None, None, None
 
 
-def _roi_pool_head_fwd(x, rois, roi_inds, ph, pw, img_h, img_w, ss, rois_sorted):
+def _roi_pool_head_fwd(x, rois, roi_inds, ph, pw, img_h, img_w, ss, rois_sorted, outs=None):
     lib = _lib.load()
     N, C, H, W = x.shape
     R = rois.size(0)
-    boxes = torch.empty((R, 5), dtype=torch.float32, device=x.device)
-    out = torch.empty((R, C, ph, pw), dtype=torch.float32, device=x.device)
-    am = torch.empty((R, C, ph, pw), dtype=torch.int32, device=x.device)
+    if outs is None:
+        boxes = torch.empty((R, 5), dtype=torch.float32, device=x.device)
+        out = torch.empty((R, C, ph, pw), dtype=torch.float32, device=x.device)
+        am = torch.empty((R, C, ph, pw), dtype=torch.int32, device=x.device)
+    else:  # caller-owned (out, argmax, boxes): no allocation on the issue path
+        out, am, boxes = outs
+        if (tuple(out.shape) != (R, C, ph, pw) or tuple(am.shape) != (R, C, ph, pw)
+                or tuple(boxes.shape) != (R, 5) or out.dtype != torch.float32
+                or am.dtype != torch.int32 or boxes.dtype != torch.float32):
+            raise RuntimeError("roi_pool_head: out buffers must be fp32 [R,C,ph,pw], int32 [R,C,ph,pw], "
+                               "fp32 [R,5]")
     ws = _lib.cached_workspace("roi_pool_fwd", lib.frcnn_roi_pool_fwd_workspace_size(R, N, C), x.device)
     _lib.check(lib.frcnn_roi_pool_fwd_head(
         _lib.ptr(x), _lib.ptr(rois), _lib.ptr(roi_inds), R, N, C, H, W, ph, pw, float(img_h),
@@ -140,13 +148,14 @@ class _RoIPoolHeadFunction(torch.autograd.Function):
 
 
 def roi_pool_head(input: torch.Tensor, rois: torch.Tensor, roi_inds: torch.Tensor, output_size,
-                  img_h, img_w, spatial_scale: float = 1.0, rois_sorted: bool = False):
+                  img_h, img_w, spatial_scale: float = 1.0, rois_sorted: bool = False, out=None):
     """ResnetHead's RoI transform + ``[idx, box]`` pack + roi_pool
     (nets/heads.py:42-48) in one call on device tensors: rois fp32 [R,4] in
     image pixels, roi_inds [R] -> (out [R,C,ph,pw], argmax int32, boxes [R,5]).
     ``rois_sorted`` promises RoIs grouped by non-decreasing image index (RPN
     proposals, train.py's sample_rois): then the transform runs inside the
-    pool kernel."""
+    pool kernel.  ``out`` = caller-owned (out, argmax, boxes) buffers
+    (inference only)."""
     if input.dim() != 4:
         raise RuntimeError("input must be [N, C, H, W]")
     if rois.dim() != 2 or rois.size(1) != 4 or roi_inds.dim() != 1 or roi_inds.size(0) != rois.size(0):
@@ -157,7 +166,9 @@ def roi_pool_head(input: torch.Tensor, rois: torch.Tensor, roi_inds: torch.Tenso
     args = (x, _to_dev(rois), _to_dev(roi_inds), int(ph), int(pw), float(img_h), float(img_w),
             float(spatial_scale), bool(rois_sorted))
     if not (torch.is_grad_enabled() and x.requires_grad):  # inference: no autograd node
-        return _roi_pool_head_fwd(*args)
+        return _roi_pool_head_fwd(*args, outs=out)
+    if out is not None:
+        raise RuntimeError("roi_pool_head: out= is for inference (no autograd)")
     return _RoIPoolHeadFunction.apply(*args)
 
 
@@ -197,6 +208,9 @@ def roi_pool(input: torch.Tensor, boxes, output_size, spatial_scale: float = 1.0
 
 
 # ------------------------------------------------------------------ proposals
+_params_cache = {}  # launch-parameter block + workspace size per layer shape (built once)
+
+
 def propose(scores: torch.Tensor, deltas: torch.Tensor, *, img_w: float, img_h: float,
             pre_nms: int, post_nms: int, nms_thresh: float = 0.7, min_size: float = 16,
             anchors: torch.Tensor = None, anchor_base: torch.Tensor = None, feat_h: int = 0,
@@ -211,16 +225,21 @@ def propose(scores: torch.Tensor, deltas: torch.Tensor, *, img_w: float, img_h: 
     lib = _lib.load()
     dev = scores.device
     N, A = scores.shape
-    p = _lib.ProposeParams()
-    p.N, p.A = N, A
-    K = 0
-    if anchors is None:
-        K = anchor_base.size(0)
-        if K * feat_h * feat_w != A:
+    K = 0 if anchors is None and anchor_base is None else (anchor_base.size(0) if anchors is None else 0)
+    key = (N, A, K, feat_h, feat_w, feat_stride, float(img_h), float(img_w), float(min_size),
+           int(pre_nms), int(post_nms), float(nms_thresh))
+    cached = _params_cache.get(key)
+    if cached is None:
+        if anchors is None and K * feat_h * feat_w != A:
             raise RuntimeError(f"A={A} != feat_h*feat_w*K={feat_h}*{feat_w}*{K}")
-    p.K, p.feat_h, p.feat_w, p.feat_stride = K, feat_h, feat_w, feat_stride
-    p.img_h, p.img_w, p.min_size = float(img_h), float(img_w), float(min_size)
-    p.pre_nms, p.post_nms, p.iou_threshold = int(pre_nms), int(post_nms), float(nms_thresh)
+        p = _lib.ProposeParams()
+        p.N, p.A = N, A
+        p.K, p.feat_h, p.feat_w, p.feat_stride = K, feat_h, feat_w, feat_stride
+        p.img_h, p.img_w, p.min_size = float(img_h), float(img_w), float(min_size)
+        p.pre_nms, p.post_nms, p.iou_threshold = int(pre_nms), int(post_nms), float(nms_thresh)
+        cached = (p, int(lib.frcnn_propose_workspace_size(p)))
+        _params_cache[key] = cached
+    p, need = cached
     if out is None:
         rois = torch.empty((N, post_nms, 4), dtype=torch.float32, device=dev)
         idx = torch.empty((N, post_nms), dtype=torch.int32, device=dev)
@@ -231,7 +250,6 @@ def propose(scores: torch.Tensor, deltas: torch.Tensor, *, img_w: float, img_h: 
                 or tuple(cnt.shape) != (N,) or rois.dtype != torch.float32
                 or idx.dtype != torch.int32 or cnt.dtype != torch.int32):
             raise RuntimeError("propose: out buffers must be fp32 [N,post,4], int32 [N,post], int32 [N]")
-    need = lib.frcnn_propose_workspace_size(p)
     ws = workspace if workspace is not None else _lib.cached_workspace("propose", need, dev)
     if ws.numel() < need:
         raise RuntimeError(f"propose: workspace of {ws.numel()} B < {need} B")

@@ -13,6 +13,7 @@ for c in cfg2 cfg4 cfg5; do
   timeout -k 10 200 python -u tools/ab_roi_pool.py --config $c --variants "$V" > "$OUT/ab_$c.log" 2>&1 || exit $?
 done
 timeout -k 10 200 python -u tools/ab_roi_pool_bwd.py > "$OUT/ab_bwd.log" 2>&1 || exit $?
+timeout -k 10 300 python -u bench.py > "$OUT/bench_cfg2.log" 2>&1 || exit $?
 if [ "${3:-}" = pmc ]; then
   bash tools/pmc_roi_pool.sh "$OUT/pmc" "${V%%,*}" cfg2 > "$OUT/pmc.log" 2>&1 || exit $?
 fi
