@@ -359,7 +359,13 @@ def train_step_fn(args, c, sc, de, x, base, first_image, ev):
     image (numpy's MT19937 stream kept on the device, sync-free, in the
     reference's order: all AT, then all PT) -> sampled RoIs fp64->fp32 ->
     RoI transform + pack + RoIPool forward -> RoIPool backward of a resident
-    upstream gradient (the head's dL/dpool)."""
+    upstream gradient (the head's dL/dpool).
+
+    With --streams 2 the step runs on three HIP streams: the target creators
+    (the device RNG stream: AT(k), PT(k), AT(k+1), ... in the reference's order)
+    on one, the proposal layer on another -- AT(k) needs only the gt boxes and
+    the anchors, so it starts before step k's proposals are done -- and the
+    RoIPool forward + backward of step k on a third, beside AT(k+1)."""
     from replication_faster_rcnn_amd import anchors as A, ops, synth, targets
     from replication_faster_rcnn_amd.utils import rng_state_to_device
     N, dev = sc.size(0), sc.device
@@ -374,8 +380,10 @@ def train_step_fn(args, c, sc, de, x, base, first_image, ev):
     gen = torch.Generator(device=dev)
     gen.manual_seed(1)
     grad = torch.randn((N * S, x.size(1), 7, 7), device=dev, generator=gen)
-    s_props, s_pool = make_streams(args)
-    s_prop = s_props[0]  # the device RNG stream orders the steps: one proposal stream
+    if args.streams == 1:
+        s_prop = s_rng = s_pool = torch.cuda.current_stream()
+    else:
+        s_prop, s_rng, s_pool = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
     state = {}
 
     def step(timed):
@@ -383,12 +391,18 @@ def train_step_fn(args, c, sc, de, x, base, first_image, ev):
             rois, _, cnt = ops.propose(sc, de, img_w=c["img_w"], img_h=c["img_h"],
                                        pre_nms=c["pre_nms"], post_nms=c["post_nms"],
                                        anchor_base=base, feat_h=c["feat_h"], feat_w=c["feat_w"])
+            prop_ready = torch.cuda.Event()
+            prop_ready.record(s_prop)
+        with torch.cuda.stream(s_rng):
             reg_t, lab = targets.anchor_targets(boxes, labels, anchors, rng=rng)
+            s_rng.wait_event(prop_ready)
+            rois.record_stream(s_rng)   # allocated on s_prop, read on s_rng
+            cnt.record_stream(s_rng)
             s_roi, s_reg, s_lab, s_cnt = targets.proposal_targets(rois, cnt, boxes, labels,
                                                                   n_sample=S, rng=rng)
             sample_rois = s_roi.float().view(-1, 4)          # train.py:86,102,107
             ready = torch.cuda.Event()
-            ready.record(s_prop)
+            ready.record(s_rng)
         with torch.cuda.stream(s_pool):
             s_pool.wait_event(ready)
             sample_rois.record_stream(s_pool)
