@@ -62,6 +62,18 @@ def parse():
     ap.add_argument("--prop-streams", type=int, default=2,
                     help="with --streams 2 (inference configs): proposal layers of consecutive "
                          "steps round-robin over this many HIP streams")
+    ap.add_argument("--prop-cus", type=int, default=0,
+                    help="with --streams 2: CUs reserved for the proposal streams (spread over the "
+                         "XCDs); the RoIPool stream gets the rest.  0 = no reservation")
+    ap.add_argument("--mask-pool", type=int, default=1, choices=(0, 1),
+                    help="with --prop-cus: 1 = the RoIPool stream is masked to the other CUs")
+    ap.add_argument("--pool-wgs", default="auto",
+                    help="RoIPool forward workgroups (frcnn_set_path roi_pool_wgs): auto = one per "
+                         "CU of its stream")
+    ap.add_argument("--propose-path", default="auto",
+                    help="frcnn_set_path propose: auto | hybrid | lazy | wide")
+    ap.add_argument("--cu-order", default="rr", choices=("rr", "blk"),
+                    help="how the CU-mask numbering maps to XCDs (tools/cu_probe.py)")
     ap.add_argument("--host-io", type=int, default=0, choices=(0, 1),
                     help="1: PCIe-inclusive variant -- each step copies its inputs (scores, "
                          "deltas, features) from pinned host memory and the rois + pooled "
@@ -263,12 +275,55 @@ def cpu_baseline(cfg, seconds, min_images, train=False):
 
 
 # ------------------------------------------------------------------ steps
+class _On:
+    """`with _On(s):` -- torch.cuda.stream(s) without its per-entry Stream
+    objects (~6 us per use on the issue path): switches torch's current stream
+    to `s` and back to `home` (the stream current when the steps were built)."""
+
+    __slots__ = ("ids", "home")
+
+    def __init__(self, s, home):
+        self.ids = (s.stream_id, s.device_index, s.device_type)
+        self.home = (home.stream_id, home.device_index, home.device_type)
+
+    def __enter__(self):
+        i, d, t = self.ids
+        torch._C._cuda_setStream(stream_id=i, device_index=d, device_type=t)
+
+    def __exit__(self, *exc):
+        i, d, t = self.home
+        torch._C._cuda_setStream(stream_id=i, device_index=d, device_type=t)
+        return False
+
+
+def reserved_cus(n, k, order):
+    """k CUs spread evenly over the 8 XCDs (hipExtStreamCreateWithCUMask
+    numbering; `order` = how that numbering maps to XCDs: "rr" = CU i on XCD
+    i % 8, "blk" = CUs 32x..32x+31 on XCD x -- tools/cu_probe.py)."""
+    per = max(1, k // 8)
+    xcd = [[i for i in range(n) if i % 8 == x] if order == "rr" else
+           [i for i in range(n) if i // (n // 8) == x] for x in range(8)]
+    return sorted(c for lst in xcd for c in lst[-per:])
+
+
 def make_streams(args):
-    """(list of proposal streams, RoIPool stream)."""
+    """(list of proposal streams, RoIPool stream).  With --prop-cus K the
+    proposal streams run on K reserved CUs (K/8 per XCD) and the RoIPool on the
+    rest: the pool's one-workgroup-per-CU tiles hold every CU's LDS for its
+    whole run, so without a reservation the next step's proposal kernels wait
+    for it; the pool sizes its grid to its stream's CUs."""
     if args.streams == 1:
         s = torch.cuda.current_stream()
         return [s], s
-    return [torch.cuda.Stream() for _ in range(max(1, args.prop_streams))], torch.cuda.Stream()
+    nps = max(1, args.prop_streams)
+    if args.prop_cus > 0:
+        from replication_faster_rcnn_amd import _lib
+        n = _lib.cu_count()
+        res = reserved_cus(n, args.prop_cus, args.cu_order)
+        rest = [i for i in range(n) if i not in set(res)]
+        pool = _lib.cu_stream(rest) if args.mask_pool else torch.cuda.Stream()
+        return [_lib.cu_stream(res) for _ in range(nps)], pool
+    return [torch.cuda.Stream() for _ in range(nps)], torch.cuda.Stream()
 
 
 def gather(rois, idx, cnt, n_total, backend):
@@ -294,6 +349,9 @@ def inference_step_fn(args, c, sc, de, x, base, world, n_total, backend, ev):
     inds = torch.arange(N, device=dev, dtype=torch.float32).repeat_interleave(post)
     s_props, s_pool = make_streams(args)
     nps = len(s_props)
+    home = torch.cuda.current_stream()
+    on_prop = [_On(sp, home) for sp in s_props]
+    on_pool = _On(s_pool, home)
     prop_out = [(torch.empty((N, post, 4), dtype=torch.float32, device=dev),
                  torch.empty((N, post), dtype=torch.int32, device=dev),
                  torch.empty((N,), dtype=torch.int32, device=dev)) for _ in range(nps)]
@@ -316,7 +374,7 @@ def inference_step_fn(args, c, sc, de, x, base, world, n_total, backend, ev):
         s_prop = s_props[j]
         k_step[0] += 1
         rois, idx, cnt = prop_out[j]
-        with torch.cuda.stream(s_prop):
+        with on_prop[j]:
             if done[j] is not None:
                 s_prop.wait_event(done[j])  # the pool that read prop_out[j] (and d_in[j]) last time
             sc_, de_, x_ = sc, de, x
@@ -332,7 +390,7 @@ def inference_step_fn(args, c, sc, de, x, base, world, n_total, backend, ev):
             if args.host_io:
                 h_rois.copy_(rois, non_blocking=True)
             ready[j].record(s_prop)
-        with torch.cuda.stream(s_pool):
+        with on_pool:
             s_pool.wait_event(ready[j])
             if timed:
                 e0, e1 = ev["pairs"][ev["i"]]
@@ -431,7 +489,10 @@ def main():
     dev = torch.device("cuda", dev_index)
     from replication_faster_rcnn_amd import _lib
     from replication_faster_rcnn_amd import anchors as A
-    _lib.set_path("roi_pool_cg", args.roi_cg)
+    for op, v in (("roi_pool_cg", args.roi_cg), ("roi_pool_wgs", args.pool_wgs),
+                  ("propose", args.propose_path)):
+        if v != "auto":
+            _lib.set_path(op, v)
     from replication_faster_rcnn_amd import dist as fdist
     from replication_faster_rcnn_amd import synth
     cfg = resolve_config(args, world)
@@ -518,6 +579,8 @@ def main():
                    "parallelism": f"dp{world} (per-image sharding)", "streams": args.streams,
                    "prop_streams": args.prop_streams if (args.streams == 2 and not train) else 1,
                    "host_io": bool(args.host_io), "roi_cg": args.roi_cg,
+                   "prop_cus": args.prop_cus if (args.streams == 2 and not train) else 0,
+                   "pool_wgs": args.pool_wgs, "propose_path": args.propose_path,
                    "collective": (None if world == 1 else
                                   ("RCCL all_gather_into_tensor" if backend == "nccl"
                                    else "gloo all_gather_into_tensor (ranks share a GPU)")),

@@ -18,7 +18,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfrcnn_mi355x.so")
+# FRCNN_LIB_PATH: A/B tools may point at another build of the same library
+LIB_PATH = os.environ.get("FRCNN_LIB_PATH") or os.path.join(_HERE, "libfrcnn_mi355x.so")
 
 P = ctypes.c_void_p
 I32 = ctypes.c_int
@@ -42,6 +43,10 @@ SIGNATURES = {
     "frcnn_last_error": (ctypes.c_char_p, []),
     "frcnn_device_cu_count": (I32, [P]),
     "frcnn_set_path": (I32, [ctypes.c_char_p, ctypes.c_char_p]),
+    "frcnn_stream_create": (I32, [P, I32, P]),
+    "frcnn_stream_destroy": (I32, [P]),
+    "frcnn_stream_cu_count": (I32, [P, P]),
+    "frcnn_probe_hw_ids": (I32, [P, I32, I32, P]),
     "frcnn_anchor_base": (I32, [P, I32, P, I32, F64, P, P]),
     "frcnn_generate_anchors": (I32, [P, I32, I32, I32, I32, P, P]),
     "frcnn_reg2bbox": (I32, [P, P, I64, P, P]),
@@ -85,6 +90,8 @@ def load(require_gpu: bool = True):
                              "(run __graft_entry__.build() or make -C replication_faster_rcnn_amd/csrc)")
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("FRCNN_LIB_PATH") and not hasattr(lib, name):
+                continue  # an older build under A/B: bind what it exports
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
@@ -104,12 +111,26 @@ def check(rc: int, what: str):
         raise FrcnnError(f"{what} failed (rc={rc}): {msg}")
 
 
-def stream_ptr(device=None):
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+_raw_stream = torch._C._cuda_getCurrentRawStream  # hipStream_t of the current torch stream (int)
+_cur_device = torch._C._cuda_getDevice
+
+
+def stream_ptr(device=None) -> int:
+    """hipStream_t (as an int, for c_void_p arguments) of torch's current
+    stream on `device` (default: the current device).  The raw torch._C
+    getters are used on the issue path: torch.cuda.current_stream() builds a
+    Stream object (~2.5 us per call)."""
+    if device is None:
+        return _raw_stream(_cur_device())
+    if isinstance(device, int):
+        return _raw_stream(device)
+    d = torch.device(device)
+    return _raw_stream(d.index if d.index is not None else _cur_device())
 
 
 def ptr(t):
-    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+    """Device address of a tensor (int) or None (NULL) for c_void_p arguments."""
+    return t.data_ptr() if t is not None else None
 
 
 def device():
@@ -129,11 +150,11 @@ def cached_workspace(tag: str, nbytes: int, dev) -> torch.Tensor:
     workspaces are stream-ordered scratch, so one buffer per stream serves every
     call on that stream (no allocation on the issue path).  Allocated while the
     stream is current, so the caching allocator orders its reuse on that stream."""
-    s = torch.cuda.current_stream(dev)
-    key = (tag, s.device_index, s.cuda_stream)
+    di = dev.index if isinstance(dev, torch.device) and dev.index is not None else _cur_device()
+    key = (tag, di, _raw_stream(di))
     ws = _ws_cache.get(key)
     if ws is None or ws.numel() < nbytes:
-        ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
+        ws = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=torch.device("cuda", di))
         _ws_cache[key] = ws
     return ws
 
@@ -142,6 +163,36 @@ def cu_count() -> int:
     lib = load()
     n = ctypes.c_int(0)
     check(lib.frcnn_device_cu_count(ctypes.byref(n)), "device_cu_count")
+    return int(n.value)
+
+
+def cu_stream(cu_mask=None) -> torch.cuda.ExternalStream:
+    """A torch stream on the CUs listed in ``cu_mask`` (iterable of CU indices,
+    hipExtStreamCreateWithCUMask numbering; None = every CU).  The HIP stream
+    lives as long as the process (frcnn_stream_destroy is left to the caller
+    via ``stream.frcnn_handle``)."""
+    lib = load()
+    h = ctypes.c_void_p(0)
+    if cu_mask is None:
+        check(lib.frcnn_stream_create(None, 0, ctypes.byref(h)), "stream_create")
+    else:
+        n = cu_count()
+        words = (ctypes.c_uint32 * ((n + 31) // 32))()
+        for c in cu_mask:
+            if not 0 <= int(c) < n:
+                raise ValueError(f"CU {c} out of range [0, {n})")
+            words[int(c) // 32] |= 1 << (int(c) % 32)
+        check(lib.frcnn_stream_create(words, len(words), ctypes.byref(h)), "stream_create")
+    s = torch.cuda.ExternalStream(h.value, device=device())
+    s.frcnn_handle = h.value
+    return s
+
+
+def stream_cu_count(stream) -> int:
+    lib = load()
+    n = ctypes.c_int(0)
+    check(lib.frcnn_stream_cu_count(ctypes.c_void_p(stream.cuda_stream), ctypes.byref(n)),
+          "stream_cu_count")
     return int(n.value)
 
 

@@ -76,6 +76,14 @@ extern "C" int frcnn_set_path(const char* op, const char* path) {
             return FRCNN_EINVAL;
         }
         g_path.roi_split = static_cast<int>(v);
+    } else if (is(op, "roi_pool_wgs")) {
+        char* end = nullptr;
+        const long v = aut ? 0 : std::strtol(path, &end, 10);
+        if (!aut && (end == path || *end != '\0' || v < 0 || v > 65535)) {
+            set_error("frcnn_set_path: roi_pool_wgs must be auto or 0..65535, got '%s'", path);
+            return FRCNN_EINVAL;
+        }
+        g_path.roi_wgs = static_cast<int>(v);
     } else if (is(op, "roi_pool_cg") && (aut || is(path, "4") || is(path, "8") || is(path, "16"))) {
         g_path.roi_cg = aut ? 0 : std::atoi(path);
     } else {
@@ -99,4 +107,89 @@ extern "C" int frcnn_device_cu_count(int* out) {
         return frcnn::check_launch("frcnn_device_cu_count");
     *out = n;
     return FRCNN_OK;
+}
+
+// ------------------------------------------------------ streams on CU subsets
+// A stream whose kernels may only use the CUs set in `cu_mask` (bit i of word
+// i/32 = CU i, hipExtStreamCreateWithCUMask numbering).  Used to run the
+// latency-bound proposal chain on a few reserved CUs beside the RoIPool, which
+// otherwise holds every CU's LDS for its whole run.
+extern "C" int frcnn_stream_create(const uint32_t* cu_mask, int words, void** out) {
+    if (!out || words < 0 || (words > 0 && !cu_mask)) {
+        frcnn::set_error("frcnn_stream_create: bad arguments");
+        return FRCNN_EINVAL;
+    }
+    hipStream_t s = nullptr;
+    const hipError_t e = words > 0 ? hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(words), cu_mask)
+                                   : hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        frcnn::set_error("frcnn_stream_create: %s", hipGetErrorString(e));
+        return FRCNN_EHIP;
+    }
+    *out = s;
+    return FRCNN_OK;
+}
+
+extern "C" int frcnn_stream_destroy(void* stream) {
+    if (stream && hipStreamDestroy(frcnn::as_stream(stream)) != hipSuccess)
+        return frcnn::check_launch("frcnn_stream_destroy");
+    return FRCNN_OK;
+}
+
+namespace frcnn {
+// CUs a kernel launched on `s` may use: popcount of the stream's CU mask
+// (every CU for the null stream and for unmasked streams).  Cached per stream
+// handle: the mask is fixed at creation.
+int stream_cu_count(hipStream_t s) {
+    const int all = device_cu_count();
+    if (!s) return all;
+    static thread_local hipStream_t c_s[8] = {};
+    static thread_local int c_n[8] = {};
+    static thread_local int c_next = 0;
+    for (int i = 0; i < 8; ++i)
+        if (c_s[i] == s) return c_n[i];
+    uint32_t m[32] = {};
+    int n = all;
+    if (hipExtStreamGetCUMask(s, 32, m) == hipSuccess) {
+        int bits = 0;
+        for (int i = 0; i < 32 && i * 32 < all; ++i) bits += __builtin_popcount(m[i]);
+        if (bits > 0 && bits < all) n = bits;
+    } else {
+        (void)hipGetLastError();
+    }
+    c_s[c_next] = s;
+    c_n[c_next] = n;
+    c_next = (c_next + 1) & 7;
+    return n;
+}
+}  // namespace frcnn
+
+extern "C" int frcnn_stream_cu_count(void* stream, int* out) {
+    if (!out) {
+        frcnn::set_error("frcnn_stream_cu_count: null pointer");
+        return FRCNN_EINVAL;
+    }
+    *out = frcnn::stream_cu_count(frcnn::as_stream(stream));
+    return FRCNN_OK;
+}
+
+// Diagnostic: where the workgroups of a launch ran.  out[2*b] = HW_ID
+// (cu_id bits 11:8, sh_id 12, se_id 15:13), out[2*b+1] = XCC_ID of workgroup b.
+__global__ void hw_id_probe_kernel(uint32_t* out, int spin) {
+    if (threadIdx.x == 0) {
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+        out[2 * blockIdx.x] = hw;
+        out[2 * blockIdx.x + 1] = xcc;
+    }
+    for (int i = 0; i < spin; ++i) __builtin_amdgcn_s_sleep(127);  // hold the CU so blocks spread
+}
+
+extern "C" int frcnn_probe_hw_ids(uint32_t* out, int nblocks, int spin, void* stream) {
+    if (!out || nblocks <= 0 || spin < 0 || spin > 4096) {
+        frcnn::set_error("frcnn_probe_hw_ids: bad arguments");
+        return FRCNN_EINVAL;
+    }
+    hipLaunchKernelGGL(hw_id_probe_kernel, dim3(nblocks), dim3(64), 0, frcnn::as_stream(stream), out, spin);
+    return frcnn::check_launch("hw_id_probe_kernel");
 }

@@ -29,11 +29,14 @@ struct PathCfg {
     int propose = kPathAuto;
     int roi_split = 0;  // RoI shares per (image, channel group); 0 = auto
     int roi_cg = 0;     // channels per RoIPool workgroup (4 / 8 / 16); 0 = auto
+    int roi_wgs = 0;    // RoIPool forward grid (workgroups); 0 = one per resident slot of the stream's CUs
 };
 const PathCfg& path_cfg();
 
 // CU count of the current device (cached after the first call).
 int device_cu_count();
+// CUs a launch on stream s may use (its CU mask; every CU if unmasked).
+int stream_cu_count(hipStream_t s);
 
 // Launch-and-check helper used by every C-ABI wrapper: returns FRCNN_EHIP
 // with the HIP message when the last launch failed.

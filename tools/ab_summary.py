@@ -11,4 +11,4 @@ for f in sorted(glob.glob(os.path.join(sys.argv[1], "ab_*.log"))):
         continue
     d = json.loads(t[t.index("{"):])
     key = "variants" if "variants" in d else "paths"
-    print(d["config"], {k: round(v["us_median"], 1) for k, v in d[key].items()})
+    print(os.path.basename(f), d["config"], {k: round(v["us_median"], 1) for k, v in d[key].items()})
