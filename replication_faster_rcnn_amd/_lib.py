@@ -47,6 +47,7 @@ SIGNATURES = {
     "frcnn_stream_destroy": (I32, [P]),
     "frcnn_stream_cu_count": (I32, [P, P]),
     "frcnn_probe_hw_ids": (I32, [P, I32, I32, P]),
+    "frcnn_debug_sampler_prof": (I32, [P, I32]),  # only in -DFRCNN_SAMPLER_PROF builds
     "frcnn_anchor_base": (I32, [P, I32, P, I32, F64, P, P]),
     "frcnn_generate_anchors": (I32, [P, I32, I32, I32, I32, P, P]),
     "frcnn_reg2bbox": (I32, [P, P, I64, P, P]),
@@ -90,8 +91,8 @@ def load(require_gpu: bool = True):
                              "(run __graft_entry__.build() or make -C replication_faster_rcnn_amd/csrc)")
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            if os.environ.get("FRCNN_LIB_PATH") and not hasattr(lib, name):
-                continue  # an older build under A/B: bind what it exports
+            if (os.environ.get("FRCNN_LIB_PATH") or name.startswith("frcnn_debug_")) and not hasattr(lib, name):
+                continue  # an A/B build (FRCNN_LIB_PATH) or a debug-only entry point
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -12,15 +12,15 @@
 // with random_interval = "next MT19937 word & mask(i), reject while > i".
 // The caller hands the MT19937 state (624 words + pos) in and gets it back,
 // so the numpy global stream continues exactly as after the reference's calls.
-//  * one 1024-thread workgroup runs the rejection automaton a whole 624-word
-//    state block at a time: thread t owns word t; which words are accepted
-//    depends on how many earlier words were, solved as a fixed point over
-//    block prefix counts (a few rounds); the twist is a 3-phase parallel
-//    update of the same block (fy_steps_block / mt_twist_block);
-//  * only the permutation positions the caller needs are reconstructed, by
-//    tracing each position backwards through the recorded swaps (lanes in
-//    parallel): the last m positions for AnchorTarget (which m elements
-//    survive the disable), the first k for ProposalTarget (in order).
+//  * one 1024-thread workgroup runs the rejection automaton over 1024-word
+//    windows of the stream: thread t owns word t; which words are accepted
+//    depends on how many earlier words were, solved as a fixed point over the
+//    16 wave prefix counts (a few rounds); state blocks are twisted into an LDS
+//    ring ahead of the window (fy_walk / mt_twist);
+//  * only the permutation positions the caller needs are reconstructed from
+//    the recorded swaps (fy_final): the last m positions for AnchorTarget
+//    (which m elements survive the disable), the first k for ProposalTarget
+//    (in order).
 #include <cfloat>
 #include <cmath>
 
@@ -259,207 +259,356 @@ __device__ __forceinline__ uint32_t mask_for(uint32_t v) {
 }
 
 // ------------------------------------------------------------ stream walker
-// The sampler kernels run as ONE 256-thread workgroup (the MT19937 stream is a
-// single sequential resource: image n's draws start where image n-1's
-// ended).  Per 624-word state block: a 3-phase parallel twist by the whole
-// workgroup, then ONE wave runs the rejection automaton over the block, 256
-// words per round (4 per lane, 4 independent ballot chains for ILP): word t's
-// step is i_cur - #accepted(words < t), accept(t) = (w_t & mask(step)) <=
-// step; starting from "all accepted", the iteration accept <- f(prefix(accept))
-// reaches the unique fixed point (word t depends only on words < t) in a few
-// rounds, since a rejection shifts later steps by one and only flips words
-// near a bound.  Measured per block (round-1 timeline probe, tools/experiments): 16 waves with a
-// barrier per round ~4 us, one wave alone ~2.6-3.3 us (issue bound), 4 waves.
-constexpr int kSampThreads = 256;
-constexpr int kSampWaves = kSampThreads / 64;  // 4: one per SIMD
-constexpr int kWpl = 3;                        // words per lane
-constexpr int kSeg = kWpl * 64;                // words per wave segment (4 x 192 >= 624)
+// The sampler kernels run as ONE 1024-thread workgroup: the MT19937 stream is a
+// single sequential resource (image n's draws start where image n-1's ended).
+//  * The raw state blocks live in an LDS ring of 3.  227 threads twist a block
+//    from the previous one, each producing words t, t + 227, t + 454 in
+//    registers (the one cross-thread input, the new word 0 that word 623
+//    wraps to, is recomputed), so a block costs one barrier.
+//  * The rejection automaton consumes the stream in windows of 1024 words,
+//    thread t owning word t: word t's step is i_cur - #accepted(words < t),
+//    accepted iff (w_t & mask(step)) <= step.  Each wave solves its 64 words
+//    exactly for an assumed count of accepted words before it (ballot fixed
+//    point), one barrier publishes the 16 wave counts, and the window is
+//    settled when no count changed: the unique fixed point, since word t
+//    depends only on words < t.  A word's decision depends on its step only
+//    when (w & mask) lies that close to it, so guesses from the expected
+//    acceptance rate settle in 2-3 rounds.
+//  * Survivors / samples are read off the recorded swaps J (fy_final).
+constexpr int kSampThreads = 1024;
+constexpr int kSampWaves = kSampThreads / 64;
+constexpr int kMaxKeep = 4096;  // recorded swaps / survivors per choice() call (LDS)
+#ifdef FRCNN_SAMPLER_PROF
+__device__ unsigned long long g_samp_prof[16];
+#define SPROF_T0() const unsigned long long _t0 = __builtin_amdgcn_s_memtime()
+#define SPROF_ADD(k, v) do { if (threadIdx.x == 0) g_samp_prof[k] += (v); } while (0)
+#define SPROF_DT(k) SPROF_ADD(k, __builtin_amdgcn_s_memtime() - _t0)
+#else
+#define SPROF_T0() do {} while (0)
+#define SPROF_ADD(k, v) do {} while (0)
+#define SPROF_DT(k) do {} while (0)
+#endif
+constexpr int kRing = 3;  // a window (<= 1024 words from pos <= 624) spans <= 3 blocks
+#ifndef FRCNN_SEQ_BELOW
+#define FRCNN_SEQ_BELOW 1024
+#endif
+constexpr int kSeqBelow = FRCNN_SEQ_BELOW;  // steps below which one wave walks the window
 
-struct StreamLds {
-    uint32_t key[kMtN];
-    __attribute__((aligned(16))) int tot[3][kSampWaves];  // segment totals, by round
-    __attribute__((aligned(16))) int last[kSampWaves];    // highest accepted word + 1
-    int pos;                                             // next unused word of key[]
+struct Stream {  // block-uniform: every thread tracks the same values
+    int slot;    // ring slot of the block numpy's key[] holds
+    int off;     // numpy's pos within it (0..624)
+    int ngen;    // blocks twisted ahead of it (0..2)
 };
 
-// numpy mt19937_gen over the whole block: new[i] depends on old[i], old[i+1]
-// and old[i+397] (i < 227) or new[i-227]; three phases of independent words.
-__device__ void mt_twist_block(StreamLds& S) {
-    const int tid = threadIdx.x;
-    auto gen = [&](int i, uint32_t nxt) {
-        const uint32_t y = (S.key[i] & 0x80000000u) | (nxt & 0x7fffffffu);
-        const uint32_t src = i < kMtN - kMtM ? S.key[i + kMtM] : S.key[i - (kMtN - kMtM)];
-        return src ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-    };
-    constexpr int kA = kMtN - kMtM;  // 227 <= kSampThreads
-    uint32_t v = 0;
-    if (tid < kA) v = gen(tid, S.key[tid + 1]);
-    __syncthreads();
-    if (tid < kA) S.key[tid] = v;
-    __syncthreads();
-    if (tid < kA) v = gen(kA + tid, S.key[kA + tid + 1]);
-    __syncthreads();
-    if (tid < kA) S.key[kA + tid] = v;
-    __syncthreads();
-    const int i3 = 2 * kA + tid;  // 454 .. 623
-    if (i3 < kMtN) v = gen(i3, i3 + 1 < kMtN ? S.key[i3 + 1] : S.key[0]);
-    __syncthreads();
-    if (i3 < kMtN) S.key[i3] = v;
-    __syncthreads();
+struct WalkLds {
+    uint32_t ring[kRing][kMtN];
+    int4 rec[2][kSampWaves];  // per wave, by round parity: (accepted words, margin down, margin up, base)
+    int last[kSampWaves];     // per wave: highest accepted word + 1
+};
+
+__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
 }
 
-// Fisher-Yates steps i = i_hi .. i_lo (descending) of one choice() call, on the
-// stream in S; for steps i >= rec_lo store J[i - rec_lo] = j.  Called by the
-// whole workgroup (block-uniform).  Per 624-word block the 4 waves (one per
-// SIMD) own 192-word segments; a round solves every segment exactly for an
-// assumed count of accepted words before it (ballot fixed point inside the
-// wave), then one barrier publishes the segment totals; the block is done when
-// no total changed.  The starting point is the expected acceptance rate, so
-// most blocks take one round.
-__device__ void fy_steps_block(StreamLds& S, int i_hi, int i_lo, int rec_lo, int* J) {
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    int i_cur = i_hi;
-    int it = 0;  // round counter: round r writes tot[r % 3], reads tot[(r + 2) % 3]
-    while (i_cur >= i_lo) {  // block-uniform: every thread tracks the same i_cur
-        if (S.pos == kMtN) {
-            mt_twist_block(S);
-            if (tid == 0) S.pos = 0;
-            __syncthreads();
+// numpy's mt19937_gen: nw = the state block after old (words i < 227 read
+// old[i + 397], later words the new word 227 before them; word 623 reads the
+// new word 0).
+__device__ __forceinline__ void mt_twist(const uint32_t* __restrict__ old, uint32_t* __restrict__ nw) {
+    const int t = threadIdx.x;
+    if (t < kMtN - kMtM) {
+        const uint32_t a = old[t + kMtM] ^ mt_mix(old[t], old[t + 1]);
+        const uint32_t b = a ^ mt_mix(old[t + 227], old[t + 228]);
+        nw[t] = a;
+        nw[t + 227] = b;
+        if (t + 454 < kMtN - 1) {
+            nw[t + 454] = b ^ mt_mix(old[t + 454], old[t + 455]);
+        } else if (t + 454 == kMtN - 1) {
+            const uint32_t n0 = old[kMtM] ^ mt_mix(old[0], old[1]);
+            nw[kMtN - 1] = b ^ mt_mix(old[kMtN - 1], n0);
         }
-        const int pos = S.pos;
-        const int cnt = kMtN - pos;
+    }
+}
+
+__device__ __forceinline__ void stream_load(WalkLds& S, Stream& st, const uint32_t* __restrict__ rng) {
+    for (int i = threadIdx.x; i < kMtN; i += kSampThreads) S.ring[0][i] = rng[i];
+    st.slot = 0;
+    st.off = static_cast<int>(rng[kMtN]);
+    st.ngen = 0;
+}
+
+__device__ __forceinline__ void stream_store(const WalkLds& S, const Stream& st, uint32_t* __restrict__ rng) {
+    for (int i = threadIdx.x; i < kMtN; i += kSampThreads) rng[i] = S.ring[st.slot][i];
+    if (threadIdx.x == 0) rng[kMtN] = static_cast<uint32_t>(st.off);
+}
+
+// Fisher-Yates steps i = i_hi .. 1 of one choice() call on the stream; for
+// steps i >= rec_lo, J[i - rec_lo] = j.  Block-uniform; ends with a barrier.
+// Inclusive prefix sum over each row of 16 lanes (DPP row shifts).
+__device__ __forceinline__ int row16_scan_add(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);  // row_shr:8
+    return x;
+}
+
+__device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int i_cur = i_hi;
+    while (i_cur >= 1) {
+        const int need = (st.off + kSampThreads - 1) / kMtN;  // blocks past st.slot this window reaches
+        {
+            SPROF_T0();
+            while (st.ngen < need) {
+                mt_twist(S.ring[(st.slot + st.ngen) % kRing], S.ring[(st.slot + st.ngen + 1) % kRing]);
+                __syncthreads();
+                ++st.ngen;
+                SPROF_ADD(1, 1);
+            }
+            SPROF_DT(2);
+        }
+        SPROF_ADD(0, 1);
+        SPROF_T0();
+        if (i_cur < kSeqBelow) {
+            // Small calls (narrow masks: a word's decision is sensitive to its exact
+            // step, so the parallel rounds cascade): wave 0 walks the window's 64-word
+            // chunks in order, each solved exactly on the known step.
+            if (wid == 0) {
+                int i_loc = i_cur, used = 0;
+                for (int c = 0; c < kSampWaves && i_loc >= 1; ++c) {
+                    const int gc = st.off + 64 * c + lane;
+                    const int bc = gc / kMtN;
+                    const uint32_t wc = mt_temper(S.ring[(st.slot + bc) % kRing][gc - bc * kMtN]);
+                    const float pa = (static_cast<float>(i_loc) + 1.0f) /
+                                     (static_cast<float>(mask_for(static_cast<uint32_t>(i_loc))) + 1.0f);
+                    const int ig0 = i_loc - static_cast<int>(static_cast<float>(lane) * pa);
+                    uint64_t ac = __ballot(ig0 >= 1 && (wc & mask_for(static_cast<uint32_t>(ig0))) <=
+                                                         static_cast<uint32_t>(ig0));
+                    int ilc;
+                    uint32_t mc;
+                    bool ak;
+                    for (;;) {
+                        const int below = static_cast<int>(__builtin_amdgcn_mbcnt_hi(
+                            static_cast<uint32_t>(ac >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(ac), 0u)));
+                        ilc = i_loc - below;
+                        const bool valid = ilc >= 1;
+                        mc = mask_for(static_cast<uint32_t>(valid ? ilc : 1));
+                        ak = valid && (wc & mc) <= static_cast<uint32_t>(ilc);
+                        const uint64_t nac = __ballot(ak);
+                        if (nac == ac) break;
+                        ac = nac;
+                    }
+                    if (ak && ilc >= rec_lo) J[ilc - rec_lo] = static_cast<int>(wc & mc);
+                    const int cntc = __popcll(ac);
+                    used = i_loc - cntc < 1 ? 64 * c + 64 - __clzll(ac) : 64 * (c + 1);
+                    i_loc -= cntc;
+                    SPROF_ADD(9, 1);
+                }
+                if (lane == 0) {
+                    S.last[0] = i_loc;
+                    S.last[1] = used;
+                }
+            }
+            __syncthreads();
+            SPROF_DT(10);
+            const int i_new = S.last[0], consumed = S.last[1];
+            i_cur = i_new;
+            st.off += consumed;
+            while (st.off > kMtN) {
+                st.off -= kMtN;
+                st.slot = (st.slot + 1) % kRing;
+                --st.ngen;
+            }
+            __syncthreads();
+            continue;
+        }
+        const int g = st.off + tid;
+        const int blk = g / kMtN;
+        const uint32_t w = mt_temper(S.ring[(st.slot + blk) % kRing][g - blk * kMtN]);
         const float p_acc = (static_cast<float>(i_cur) + 1.0f) /
                             (static_cast<float>(mask_for(static_cast<uint32_t>(i_cur))) + 1.0f);
-        auto guess_before = [&](int v) { return static_cast<int>(static_cast<float>(v * kSeg) * p_acc); };
-        uint32_t w[kWpl];
-        uint64_t bal[kWpl];
-        int base = guess_before(wid);
-#pragma unroll
-        for (int q = 0; q < kWpl; ++q) {
-            const int t = wid * kSeg + q * 64 + lane;
-            w[q] = t < cnt ? mt_temper(S.key[pos + t]) : 0u;
-            const int ig = i_cur - static_cast<int>(static_cast<float>(t) * p_acc);
-            const bool v0 = t < cnt && ig >= i_lo;
-            bal[q] = __ballot(v0 && (w[q] & mask_for(static_cast<uint32_t>(ig))) <=
-                                         static_cast<uint32_t>(ig));
+        auto guess = [&](int v) { return static_cast<int>(static_cast<float>(v * 64) * p_acc); };
+        int base = guess(wid);
+        uint64_t acc;
+        {
+            const int ig = i_cur - base - static_cast<int>(static_cast<float>(lane) * p_acc);
+            acc = __ballot(ig >= 1 && (w & mask_for(static_cast<uint32_t>(ig))) <= static_cast<uint32_t>(ig));
         }
-        if (tid < kSampWaves)  // "previous" totals consistent with the guessed bases
-            S.tot[(it + 2) % 3][tid] = guess_before(tid + 1) - guess_before(tid);
-        __syncthreads();
-        int il[kWpl];
-        uint32_t m[kWpl];
-        bool a[kWpl];
-        int total = 0;
-        for (;;) {
-            for (;;) {  // this segment, exact for the assumed `base`
-                int b = base;
-#pragma unroll
-                for (int q = 0; q < kWpl; ++q) {
-                    const int t = wid * kSeg + q * 64 + lane;
-                    il[q] = i_cur - b - __popcll(bal[q] & lanemask_lt());
-                    const bool valid = t < cnt && il[q] >= i_lo;
-                    m[q] = valid ? mask_for(static_cast<uint32_t>(il[q])) : 0u;
-                    a[q] = valid && (w[q] & m[q]) <= static_cast<uint32_t>(il[q]);
-                    b += __popcll(bal[q]);
+        // Round: each unsettled wave solves its 64 words for its assumed base and
+        // publishes (count, margins, base): its pattern stays exact for any base in
+        // [base - up, base + down] (no word changes its decision or mask width).
+        // The first wave whose exact base (prefix of the counts before it) falls
+        // outside its margins, and every wave after it, re-solves next round with
+        // the new prefix; the waves before it are settled.  Counts hardly depend on
+        // the base, so the second round's bases are nearly exact and most windows
+        // settle there; each round settles at least one more wave.
+        int il = 0, total = 0, par = 0;
+        uint32_t m = 0;
+        bool a = false, done = false;
+        for (int round = 0;; ++round) {
+            if (!done) {
+                for (;;) {  // this wave's 64 words, exact for the assumed `base`
+                    const int below = static_cast<int>(__builtin_amdgcn_mbcnt_hi(
+                        static_cast<uint32_t>(acc >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(acc), 0u)));
+                    il = i_cur - base - below;
+                    const bool valid = il >= 1;
+                    m = mask_for(static_cast<uint32_t>(valid ? il : 1));
+                    a = valid && (w & m) <= static_cast<uint32_t>(il);
+                    const uint64_t nacc = __ballot(a);
+                    if (nacc == acc) break;
+                    acc = nacc;
                 }
-                bool same = true;
-#pragma unroll
-                for (int q = 0; q < kWpl; ++q) {
-                    const uint64_t nb = __ballot(a[q]);
-                    same = same && nb == bal[q];
-                    bal[q] = nb;
-                }
-                if (same) break;
             }
-            int mine = 0;
-#pragma unroll
-            for (int q = 0; q < kWpl; ++q) mine += __popcll(bal[q]);
-            if (lane == 0) S.tot[it % 3][wid] = mine;
+            // Margins only from the second round on: the first round's bases are
+            // guesses, so it settles just the waves whose guess was exact (d == 0);
+            // settled waves keep d == 0 and need none either.
+            uint32_t dn = 0, up = 0;
+            if (round > 0 && !done) {
+                if (il < 1) {
+                    dn = 0x3fffffffu;
+                    up = static_cast<uint32_t>(-il);
+                } else {
+                    const uint32_t lo = (m >> 1) + 1u;  // 2^k of the mask m = 2^(k+1) - 1
+                    const uint32_t v = w & m;
+                    const uint32_t u = static_cast<uint32_t>(il);
+                    dn = a ? u - (v > lo ? v : lo) : u - lo;
+                    up = a ? m - u : v - 1u - u;
+                }
+                dn = __ockl_wfred_min_u32(dn);
+                up = __ockl_wfred_min_u32(up);
+            }
+            if (lane == 0)
+                S.rec[par][wid] = make_int4(__popcll(acc), static_cast<int>(dn), static_cast<int>(up), base);
             __syncthreads();
-            const int4 cur = *reinterpret_cast<const int4*>(S.tot[it % 3]);
-            const int4 prv = *reinterpret_cast<const int4*>(S.tot[(it + 2) % 3]);
-            ++it;
-            const int c4[4] = {cur.x, cur.y, cur.z, cur.w};
-            base = 0;
-            total = 0;
-#pragma unroll
-            for (int v = 0; v < kSampWaves; ++v) {
-                base += v < wid ? c4[v] : 0;
-                total += c4[v];
+            const int4 r = lane < kSampWaves ? S.rec[par][lane] : make_int4(0, 0, 0, 0);
+            const int incl = row16_scan_add(r.x);  // lanes 0..15: prefix over waves
+            const int excl = incl - r.x;
+            const int d = excl - r.w;  // exact base - assumed base of wave `lane`
+            const uint64_t bad = __ballot(lane < kSampWaves && (d > r.y || -d > r.z));
+            const int first_bad = bad ? __ffsll(static_cast<unsigned long long>(bad)) - 1 : kSampWaves;
+            const int my_excl = __builtin_amdgcn_readlane(excl, wid);
+            if (wid < first_bad) {
+                if (!done) {  // settled: same pattern at the exact base, steps shifted
+                    il -= my_excl - base;
+                    base = my_excl;
+                    done = true;
+                }
+            } else {
+                base = my_excl;
             }
-            if (cur.x == prv.x && cur.y == prv.y && cur.z == prv.z && cur.w == prv.w) break;
+            total = __builtin_amdgcn_readlane(incl, kSampWaves - 1);
+            par ^= 1;
+            SPROF_ADD(3, 1);
+            if (first_bad == kSampWaves) break;
         }
-        // the fixed point: il / m / a are consistent with the final bases
-#pragma unroll
-        for (int q = 0; q < kWpl; ++q)
-            if (a[q] && il[q] >= rec_lo) J[il[q] - rec_lo] = static_cast<int>(w[q] & m[q]);
-        int consumed = cnt;
-        if (i_cur - total < i_lo) {  // the call ends inside this block
-            int last = 0;
-#pragma unroll
-            for (int q = 0; q < kWpl; ++q)
-                if (bal[q]) last = wid * kSeg + q * 64 + 64 - __clzll(bal[q]);
-            if (lane == 0) S.last[wid] = last;
+        SPROF_DT(4);
+        if (a && il >= rec_lo) J[il - rec_lo] = static_cast<int>(w & m);
+        int consumed = kSampThreads;
+        if (i_cur - total < 1) {  // the call ends inside this window
+            if (lane == 0) S.last[wid] = acc ? 64 * wid + 64 - __clzll(acc) : 0;
             __syncthreads();
-            const int4 l4 = *reinterpret_cast<const int4*>(S.last);
-            consumed = max(max(l4.x, l4.y), max(l4.z, l4.w));
+            consumed = static_cast<int>(__ockl_wfred_max_u32(lane < kSampWaves ? static_cast<uint32_t>(S.last[lane]) : 0u));
         }
         i_cur -= total;
-        __syncthreads();  // everyone has read S.pos / S.last / the totals
-        if (tid == 0) S.pos = pos + consumed;
-        __syncthreads();
+        st.off += consumed;
+        while (st.off > kMtN) {  // pos == 624 stays in its block, like numpy
+            st.off -= kMtN;
+            st.slot = (st.slot + 1) % kRing;
+            --st.ngen;
+        }
+        __syncthreads();  // this window's reads of S done before the next twist / counts
     }
 }
 
-// Final value at permutation position p (identity start), given J[i - rec_lo]
-// for every step i >= rec_lo of the n-element shuffle.  Requires p >= rec_lo.
-// J must be 16-byte aligned: the swaps are read four at a time (ds_read_b128),
-// so a thread has 4 independent LDS reads in flight per 4 steps instead of one
-// dependent read per step (the ProposalTarget trace runs ~600 steps per
-// position).
-__device__ __forceinline__ int fy_trace(int p, int n, int rec_lo, const int* J) {
-    int cur = p;
-    int i = p > 1 ? p : 1;
-    for (; i < n && ((i - rec_lo) & 3); ++i) {
-        const int j = J[i - rec_lo];
-        cur = cur == i ? j : (cur == j ? i : cur);
-    }
-    const int4* J4 = reinterpret_cast<const int4*>(J + (i - rec_lo));
-    for (; i + 16 <= n; i += 16, J4 += 4) {
-        int4 q[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) q[u] = J4[u];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int b = i + 4 * u;
-            cur = cur == b ? q[u].x : (cur == q[u].x ? b : cur);
-            cur = cur == b + 1 ? q[u].y : (cur == q[u].y ? b + 1 : cur);
-            cur = cur == b + 2 ? q[u].z : (cur == q[u].z ? b + 2 : cur);
-            cur = cur == b + 3 ? q[u].w : (cur == q[u].w ? b + 3 : cur);
+// Final values at permutation positions [p_lo, p_hi) of the cnt-element
+// shuffle whose swaps J[i - rec_lo] are recorded for steps i >= rec_lo
+// (p_lo >= rec_lo, or p_lo == 0 with rec_lo == 1).  Tracing backwards in
+// time: position p takes, at step p, the value position J[p] holds then, and
+// position x's value before step t is the one position i* held before step i*,
+// i* = min{i > t : J[i] == x} (its last swap), or x itself.  So
+//   v(p) = chase(J[p], X[p]),   X[p] = min{i > p : J[i] == J[p]},
+//   chase(x, i): while i exists: x = i, i = F[i],   F[v] = min{i > v : J[i] == v}.
+// F (atomicMin, indexed from p_lo) and the steps bucketed by value (1024
+// buckets of 16, value & 1023) live in LDS; X[p] is the smallest bucket entry
+// past p with p's value (a full scan of J when the bucket overflowed: value v
+// recurs ~ln(cnt / v) times, so only the smallest values come close).
+constexpr int kBuckets = 1024;
+constexpr int kBucketCap = 16;
+struct FinalLds {
+    int F[kMaxKeep];
+    int bcnt[kBuckets];
+    int bkt[kBuckets][kBucketCap];
+};
+
+template <class Emit>
+__device__ void fy_final(int cnt, int rec_lo, int p_lo, int p_hi, const int* J, FinalLds& L, Emit emit) {
+    const int tid = threadIdx.x;
+    SPROF_T0();
+    const int f0 = p_lo;  // every chased index is >= p_lo (p_lo == 0 only when rec_lo == 1)
+    constexpr int kNone = 0x7fffffff;
+    for (int v = f0 + tid; v < cnt; v += kSampThreads) L.F[v - f0] = kNone;
+    for (int b = tid; b < kBuckets; b += kSampThreads) L.bcnt[b] = 0;
+    __syncthreads();
+    const int q0 = max(p_lo, 1);  // positions with a first query X[p]
+    for (int i = rec_lo + tid; i < cnt; i += kSampThreads) {
+        const int v = J[i - rec_lo];
+        if (v < i && v >= f0) atomicMin(&L.F[v - f0], i);
+        if (i > q0) {
+            const int b = v & (kBuckets - 1);
+            const int slot = atomicAdd(&L.bcnt[b], 1);
+            if (slot < kBucketCap) L.bkt[b][slot] = i;
         }
     }
-    for (; i < n; ++i) {
-        const int j = J[i - rec_lo];
-        cur = cur == i ? j : (cur == j ? i : cur);
+    __syncthreads();
+    for (int p = p_lo + tid; p < p_hi; p += kSampThreads) {
+        int x = 0, i;
+        if (p == 0) {
+            i = L.F[0];
+        } else {
+            x = J[p - rec_lo];
+            const int b = x & (kBuckets - 1);
+            const int n = L.bcnt[b];
+            i = kNone;
+            if (n <= kBucketCap) {
+                for (int s = 0; s < n; ++s) {
+                    const int t = L.bkt[b][s];
+                    if (t > p && t < i && J[t - rec_lo] == x) i = t;
+                }
+            } else {
+                for (int t = p + 1; t < cnt; ++t)
+                    if (J[t - rec_lo] == x) {
+                        i = t;
+                        break;
+                    }
+            }
+        }
+        while (i < cnt) {
+            x = i;
+            i = L.F[i - f0];
+        }
+        emit(p, x);
     }
-    return cur;
+    __syncthreads();
+    SPROF_DT(5);
 }
 
 // ---------------------------------------------------------- AnchorTarget RNG
 // One workgroup: for each image in order, the two choice() calls of
 // utils/utils.py:190-202.  Kept anchors are marked in keep[n][a] (zeroed by
 // the caller); pos_sampled / neg_sampled record whether a call happened.
-constexpr int kMaxKeep = 4096;
 
 __global__ __launch_bounds__(kSampThreads) void at_sample_kernel(
     int N, int A, int n_sample, int n_pos_max, const int* __restrict__ pos_list,
     const int* __restrict__ neg_list, const int* __restrict__ npos, const int* __restrict__ nneg,
     uint32_t* __restrict__ rng, uint8_t* __restrict__ keep, int* __restrict__ sampled) {
-    __shared__ StreamLds S;
-    __shared__ __attribute__((aligned(16))) int J[kMaxKeep];
-    const int tid = threadIdx.x;
-    for (int i = tid; i < kMtN; i += kSampThreads) S.key[i] = rng[i];
-    if (tid == 0) S.pos = static_cast<int>(rng[kMtN]);
+    __shared__ WalkLds S;
+    __shared__ int J[kMaxKeep];
+    __shared__ FinalLds FL;
+    SPROF_T0();
+    Stream st;
+    stream_load(S, st, rng);
     __syncthreads();
     for (int n = 0; n < N; ++n) {
         const int P = npos[n];
@@ -470,21 +619,18 @@ __global__ __launch_bounds__(kSampThreads) void at_sample_kernel(
             const int cnt = call == 0 ? P : Q;
             const int m = call == 0 ? n_pos_max : neg_keep;  // survivors
             const bool do_call = cnt > m;
-            if (tid == 0) sampled[2 * n + call] = do_call ? 1 : 0;
+            if (threadIdx.x == 0) sampled[2 * n + call] = do_call ? 1 : 0;
             if (!do_call) continue;
             const int k = cnt - m;  // disabled = perm[:k]; survivors = perm[k:]
-            fy_steps_block(S, cnt - 1, 1, k, J);
-            __syncthreads();
+            fy_walk(S, st, cnt - 1, k, J);
+            SPROF_ADD(7, cnt);
             const int* lst = (call == 0 ? pos_list : neg_list) + static_cast<size_t>(n) * A;
-            for (int p = k + tid; p < cnt; p += kSampThreads) {  // survivors, any order
-                const int v = fy_trace(p, cnt, k, J);  // p >= k >= 1
-                keep[static_cast<size_t>(n) * A + lst[v]] = 1;
-            }
-            __syncthreads();
+            uint8_t* kp = keep + static_cast<size_t>(n) * A;
+            fy_final(cnt, k, k, cnt, J, FL, [&](int, int v) { kp[lst[v]] = 1; });  // k >= 1
         }
     }
-    for (int i = tid; i < kMtN; i += kSampThreads) rng[i] = S.key[i];
-    if (tid == 0) rng[kMtN] = static_cast<uint32_t>(S.pos);
+    stream_store(S, st, rng);
+    SPROF_DT(6);
 }
 
 // grid (ceil(A/256), N): final label (after disabling) and regression target
@@ -612,11 +758,11 @@ __global__ __launch_bounds__(kSampThreads) void pt_sample_kernel(
     const int* __restrict__ neg_list, const int* __restrict__ npos, const int* __restrict__ nneg,
     uint32_t* __restrict__ rng, int* __restrict__ sample, int* __restrict__ scount,
     int* __restrict__ spos) {
-    __shared__ StreamLds S;
-    __shared__ __attribute__((aligned(16))) int J[kMaxKeep];
-    const int tid = threadIdx.x;
-    for (int i = tid; i < kMtN; i += kSampThreads) S.key[i] = rng[i];
-    if (tid == 0) S.pos = static_cast<int>(rng[kMtN]);
+    __shared__ WalkLds S;
+    __shared__ int J[kMaxKeep];
+    __shared__ FinalLds FL;
+    Stream st;
+    stream_load(S, st, rng);
     __syncthreads();
     for (int n = 0; n < N; ++n) {
         const int P = npos[n], Q = nneg[n];
@@ -629,19 +775,17 @@ __global__ __launch_bounds__(kSampThreads) void pt_sample_kernel(
             const int k = call == 0 ? kp : kn;
             const int off = call == 0 ? 0 : kp;
             if (cnt == 0) continue;
-            fy_steps_block(S, cnt - 1, 1, 1, J);  // every step: J[i-1]
-            __syncthreads();
+            fy_walk(S, st, cnt - 1, 1, J);  // every step: J[i - 1]
             const int* lst = (call == 0 ? pos_list : neg_list) + static_cast<size_t>(n) * stride;
-            for (int p = tid; p < k; p += kSampThreads) out[off + p] = lst[fy_trace(p, cnt, 1, J)];
-            __syncthreads();
+            fy_final(cnt, 1, 0, k, J, FL, [&](int p, int v) { out[off + p] = lst[v]; });
+            SPROF_ADD(8, 1);
         }
-        if (tid == 0) {
+        if (threadIdx.x == 0) {
             scount[n] = kp + kn;
             spos[n] = kp;
         }
     }
-    for (int i = tid; i < kMtN; i += kSampThreads) rng[i] = S.key[i];
-    if (tid == 0) rng[kMtN] = static_cast<uint32_t>(S.pos);
+    stream_store(S, st, rng);
 }
 
 // grid N x n_sample: sample_roi, normalised gt_roi_reg and gt_roi_label
@@ -791,6 +935,17 @@ AtWs carve_at(void* ws, int N, int A, int Gp) {
     return w;
 }
 }  // namespace
+
+#ifdef FRCNN_SAMPLER_PROF
+extern "C" int frcnn_debug_sampler_prof(unsigned long long* out, int reset) {
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_samp_prof), sizeof(unsigned long long) * 16);
+    if (reset) {
+        unsigned long long z[16] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_samp_prof), z, sizeof(z));
+    }
+    return 0;
+}
+#endif
 
 extern "C" size_t frcnn_anchor_target_workspace_size(int N, int A, int G) {
     if (N <= 0 || A <= 0 || G < 0) return 0;
