@@ -47,7 +47,6 @@ SIGNATURES = {
     "frcnn_stream_destroy": (I32, [P]),
     "frcnn_stream_cu_count": (I32, [P, P]),
     "frcnn_probe_hw_ids": (I32, [P, I32, I32, P]),
-    "frcnn_debug_sampler_prof": (I32, [P, I32]),  # only in -DFRCNN_SAMPLER_PROF builds
     "frcnn_anchor_base": (I32, [P, I32, P, I32, F64, P, P]),
     "frcnn_generate_anchors": (I32, [P, I32, I32, I32, I32, P, P]),
     "frcnn_reg2bbox": (I32, [P, P, I64, P, P]),
@@ -73,6 +72,11 @@ SIGNATURES = {
                                     P, P, P, P, P, SZ, P]),
 }
 
+# diagnostic entry points of instrumented builds only (not in include/frcnn_capi.h)
+DEBUG_SIGNATURES = {
+    "frcnn_debug_sampler_prof": (I32, [P, I32]),  # -DFRCNN_SAMPLER_PROF (tools/probe_sampler.py)
+}
+
 _lib = None
 _gpu_checked = False
 
@@ -91,11 +95,16 @@ def load(require_gpu: bool = True):
                              "(run __graft_entry__.build() or make -C replication_faster_rcnn_amd/csrc)")
         lib = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
-            if (os.environ.get("FRCNN_LIB_PATH") or name.startswith("frcnn_debug_")) and not hasattr(lib, name):
-                continue  # an A/B build (FRCNN_LIB_PATH) or a debug-only entry point
+            if os.environ.get("FRCNN_LIB_PATH") and not hasattr(lib, name):
+                continue  # an older build under A/B: bind what it exports
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        for name, (res, args) in DEBUG_SIGNATURES.items():
+            if hasattr(lib, name):
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
         _lib = lib
     global _gpu_checked
     if require_gpu and not _gpu_checked:
