@@ -67,9 +67,6 @@ def parse():
                          "XCDs); the RoIPool stream gets the rest.  0 = no reservation")
     ap.add_argument("--mask-pool", type=int, default=1, choices=(0, 1),
                     help="with --prop-cus: 1 = the RoIPool stream is masked to the other CUs")
-    ap.add_argument("--pool-wgs", default="auto",
-                    help="RoIPool forward workgroups (frcnn_set_path roi_pool_wgs): auto = one per "
-                         "CU of its stream")
     ap.add_argument("--propose-path", default="auto",
                     help="frcnn_set_path propose: auto | hybrid | lazy | wide")
     ap.add_argument("--cu-order", default="rr", choices=("rr", "blk"),
@@ -489,8 +486,7 @@ def main():
     dev = torch.device("cuda", dev_index)
     from replication_faster_rcnn_amd import _lib
     from replication_faster_rcnn_amd import anchors as A
-    for op, v in (("roi_pool_cg", args.roi_cg), ("roi_pool_wgs", args.pool_wgs),
-                  ("propose", args.propose_path)):
+    for op, v in (("roi_pool_cg", args.roi_cg), ("propose", args.propose_path)):
         if v != "auto":
             _lib.set_path(op, v)
     from replication_faster_rcnn_amd import dist as fdist
@@ -580,7 +576,7 @@ def main():
                    "prop_streams": args.prop_streams if (args.streams == 2 and not train) else 1,
                    "host_io": bool(args.host_io), "roi_cg": args.roi_cg,
                    "prop_cus": args.prop_cus if (args.streams == 2 and not train) else 0,
-                   "pool_wgs": args.pool_wgs, "propose_path": args.propose_path,
+                   "propose_path": args.propose_path,
                    "collective": (None if world == 1 else
                                   ("RCCL all_gather_into_tensor" if backend == "nccl"
                                    else "gloo all_gather_into_tensor (ranks share a GPU)")),

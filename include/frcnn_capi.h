@@ -42,7 +42,7 @@ int frcnn_device_cu_count(int* out);
  * CU i; words = 0 -> an ordinary non-blocking stream).  The proposal chain is
  * latency bound on a few workgroups while the RoIPool forward holds every CU's
  * LDS for its whole run; giving each its own CUs lets them overlap.  The
- * RoIPool forward sizes its grid to the CUs of the stream it is launched on.
+ * RoIPool forward sizes its RoI shares to the CUs of the stream it is launched on.
  * frcnn_stream_cu_count: CUs a launch on `stream` may use.
  * frcnn_probe_hw_ids: diagnostic -- out[2b] = HW_ID, out[2b+1] = XCC_ID of
  * workgroup b of an nblocks launch (spin: s_sleep rounds that keep it resident). */
@@ -60,8 +60,6 @@ int frcnn_probe_hw_ids(uint32_t* out, int nblocks, int spin, void* stream);
  *   "propose"        : "auto" | "hybrid" | "lazy" (fused per image) | "wide" (chip-wide bitmask)
  *   "roi_pool_split" : "auto" | "1".."64" (RoI shares per image and channel group)
  *   "roi_pool_cg"    : "auto" | "4" | "8" | "16" (channels per RoIPool forward workgroup)
- *   "roi_pool_wgs"   : "auto" | "1".."65535" (RoIPool forward workgroups; auto = one per resident
- *                      slot of the launch stream's CUs -- fewer leaves CUs to concurrent streams)
  * All paths give bit-identical results.  Not thread-safe against calls in
  * flight on other threads; set it before launching. */
 int frcnn_set_path(const char* op, const char* path);

@@ -76,14 +76,6 @@ extern "C" int frcnn_set_path(const char* op, const char* path) {
             return FRCNN_EINVAL;
         }
         g_path.roi_split = static_cast<int>(v);
-    } else if (is(op, "roi_pool_wgs")) {
-        char* end = nullptr;
-        const long v = aut ? 0 : std::strtol(path, &end, 10);
-        if (!aut && (end == path || *end != '\0' || v < 0 || v > 65535)) {
-            set_error("frcnn_set_path: roi_pool_wgs must be auto or 0..65535, got '%s'", path);
-            return FRCNN_EINVAL;
-        }
-        g_path.roi_wgs = static_cast<int>(v);
     } else if (is(op, "roi_pool_cg") && (aut || is(path, "4") || is(path, "8") || is(path, "16"))) {
         g_path.roi_cg = aut ? 0 : std::atoi(path);
     } else {

@@ -29,7 +29,6 @@ struct PathCfg {
     int propose = kPathAuto;
     int roi_split = 0;  // RoI shares per (image, channel group); 0 = auto
     int roi_cg = 0;     // channels per RoIPool workgroup (4 / 8 / 16); 0 = auto
-    int roi_wgs = 0;    // RoIPool forward grid (workgroups); 0 = one per resident slot of the stream's CUs
 };
 const PathCfg& path_cfg();
 

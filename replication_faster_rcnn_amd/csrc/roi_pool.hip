@@ -189,44 +189,6 @@ __device__ __forceinline__ int2 roi_range_sorted(const float* __restrict__ rois,
     return res;
 }
 
-// Counts of RoIs (grouped by non-decreasing batch index) with batch index < t.x,
-// < t.y, < t.z, < t.w, in one pass.  `red` holds 4 ints per wave.
-template <int NT>
-__device__ __forceinline__ int4 roi_counts4(const float* __restrict__ rois, int R, int4 t, int* red,
-                                            int stride) {
-    int4 c = make_int4(0, 0, 0, 0);
-    for (int r = threadIdx.x; r < R; r += NT) {
-        const int rb = static_cast<int>(rois[static_cast<size_t>(r) * stride]);
-        c.x += rb < t.x;
-        c.y += rb < t.y;
-        c.z += rb < t.z;
-        c.w += rb < t.w;
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        c.x += __shfl_xor(c.x, o, 64);
-        c.y += __shfl_xor(c.y, o, 64);
-        c.z += __shfl_xor(c.z, o, 64);
-        c.w += __shfl_xor(c.w, o, 64);
-    }
-    const int wid = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-        red[4 * wid] = c.x;
-        red[4 * wid + 1] = c.y;
-        red[4 * wid + 2] = c.z;
-        red[4 * wid + 3] = c.w;
-    }
-    __syncthreads();
-    int4 res = make_int4(0, 0, 0, 0);
-    for (int w = 0; w < NT / 64; ++w) {
-        res.x += red[4 * w];
-        res.y += red[4 * w + 1];
-        res.z += red[4 * w + 2];
-        res.w += red[4 * w + 3];
-    }
-    __syncthreads();  // red is reused by the caller
-    return res;
-}
-
 // The head's RoI transform + [idx, box] pack (nets/heads.py:42-47), fused into
 // the forward: `rois` are then [R,4] image-pixel boxes, `inds` their image index.
 struct HeadArgs {
@@ -273,7 +235,8 @@ __device__ __forceinline__ int2 geom_class(const RoiGeom& g, int H, int W, int P
 //   geo   cap x int4 (sh, sw, bh bits, bw bits)   rid cap x int (RoI index)
 //   ord   cap x int (item order)                  key cap x u8 (window class)
 //   hist  256 x u32,  misc 64 x int
-// Grid (C/CG, N [+1 when !LIST: RoIs with an out-of-range batch index], split).
+// Grid (C/CG, split, N [+1 when !LIST: RoIs with an out-of-range batch index]):
+// the image index is slowest, so row N is dispatched after every real workgroup.
 // LIST: RoIs in any order, per-image lists from roi_lists_kernel; else RoIs
 // grouped by non-decreasing batch index (each workgroup finds its image's range).
 constexpr int kDenseMisc = 64;
@@ -290,12 +253,12 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_dense_kernel(
     extern __shared__ __attribute__((aligned(16))) float4 q4[];
     const int PH = FIX ? FIX : PH_, PW = FIX ? FIX : PW_;
     const int PHW = PH * PW;
-    const int b = blockIdx.y;
+    const int b = blockIdx.z;
     const int c0 = blockIdx.x * CG;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int HW = H * W;
     const int HWs = (HW + 15) & ~15;
-    const int split = gridDim.z, z = blockIdx.z;
+    const int split = gridDim.y, z = blockIdx.y;
     int4* s_geo = reinterpret_cast<int4*>(q4 + NP * HWs);
     int* s_rid = reinterpret_cast<int*>(s_geo + cap);
     int* s_ord = s_rid + cap;
@@ -318,7 +281,7 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_dense_kernel(
         nr = cnt[b];
         lst = list + static_cast<size_t>(b) * R;
     } else {
-        const int N = gridDim.y - 1;
+        const int N = gridDim.z - 1;
         if (b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
             const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, 0, N, s_misc, 1)
                                  : roi_range_sorted<NT>(rois, R, 0, N, s_misc);
@@ -558,220 +521,175 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_dense_kernel(
 }
 
 // Tile layout of the wave-per-RoI forward: 16-pixel groups, the group's NP
-// 4-channel planes back to back -- pixel p of plane q at float4
-// (p >> 4) * NP * 16 + q * 16 + (p & 15): a ds_read_b128 of 16 lanes hits 16
-// distinct bank slots when their pixels differ mod 16, and the planes of one
-// pixel are 256 B apart (LDS immediate offsets).  The scan walks p16 = 16 * p
-// and forms the byte offset in 3 VALU (tile_off16).
+// 4-channel planes back to back (pixel p of plane q at float4
+// (g*NP + q)*16 + s, g = p >> 4), the slot s = (p ^ g) & 15 XOR-swizzled so
+// that a ds_read_b128 of bins a bin width apart does not collide, and the
+// planes of one pixel 256 B apart -- LDS immediate offsets.
 template <int NP>
 __device__ __forceinline__ const float4* tile_px(const float4* q4, int p) {
-    return q4 + (p >> 4) * (NP * 16) + (p & 15);
-}
-template <int NP>
-__device__ __forceinline__ int tile_off16(int p16) {
-    constexpr int kL = NP == 4 ? 2 : (NP == 2 ? 1 : 0);
-    return ((p16 << kL) & ~(NP * 256 - 1)) | (p16 & 0xF0);
+    const int g = p >> 4;
+    return q4 + g * (NP * 16) + ((p ^ g) & 15);
 }
 
 // ------------------------------------------------- wave-per-RoI forward
-// The default forward for RoIs grouped by image.  Work units are (channel
-// group, RoI) pairs, channel-group major, RoIs in their (image-grouped) order.
-// The 1-D grid has one workgroup per CU the launch stream may use (its CU
-// mask); workgroup g takes the contiguous unit range [g'U/G, (g'+1)U/G), where
-// g' renumbers the grid XCD-major (workgroups g, g+8, ... run on one XCD), so
-// the ranges that share an image's planes sit on one XCD and share its L2.  A
-// range is cut into segments of one (channel group, image): the segment's CG
-// channel planes are staged once into LDS (tile_px layout), then one wave per
-// RoI, lane = bin: each lane walks its window once and updates CG (max, first
-// index) pairs with torchvision's strict '>' -- the RoI geometry, the window
-// walk and the pixel address are shared by CG channels.  Waves pull RoIs from
-// an LDS counter (RoI sizes vary 100x); the geometry of a chunk of RoIs is
-// computed once per workgroup into LDS.  Output: per channel, the 49 lanes
-// write one contiguous 196-B run.  RoIs whose batch index is outside [0, N)
-// (they sort to the ends) get 0 / -1.
+// The default forward for RoIs grouped by image.  Grid (C/CG, split, N + 1):
+// one 1024-thread workgroup owns CG channel planes of one image (staged once
+// into LDS, tile_px layout) and a strided
+// share of that image's RoIs (items z, z+split, ...: RoI sizes are
+// uncorrelated with rank, so every share sees the image's size mix).  One
+// wave per RoI, lane = bin: each lane walks its window once and updates CG
+// (max, first index) pairs with torchvision's strict '>' -- the RoI geometry,
+// the window walk and the pixel address are shared by CG channels.  Waves pull
+// RoIs from an LDS counter (RoI sizes vary 100x); the RoI geometry of a chunk
+// of RoIs is computed once per workgroup into LDS.  Output: per channel, the
+// 49 lanes write one contiguous 196-B run.
 // HEAD: fused with the head's RoI transform (nets/heads.py:42-47): `rois` are
 // the [R,4] image boxes, hd.inds their image index; the [idx, box] rows are
-// formed in registers and (channel group 0) written to hd.boxes.
+// formed in registers and (channel group 0) written to hd.boxes.  The image
+// index is the slowest grid dimension, so the workgroups of row N (RoIs with a
+// batch index outside [0, N): usually none, they exit at once) are dispatched
+// after every real one instead of holding CUs between them.
 // (Measured alternatives -- RoI bins packed 64 per wave, bins sorted by window
 // shape per image or per RoI block -- are slower: DESIGN.md §3.)
 template <int NT, int CG, bool HEAD>
 __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
-    const float* __restrict__ x, const float* __restrict__ rois, int R, int N, int C, int H, int W, int PH,
-    int PW, float ss, float* __restrict__ out, int32_t* __restrict__ argmax, int geo_cap, HeadArgs hd) {
+    const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W, int PH, int PW,
+    float ss, float* __restrict__ out, int32_t* __restrict__ argmax, int geo_cap, HeadArgs hd) {
     constexpr int NP = CG / 4;
     extern __shared__ __attribute__((aligned(16))) float4 q4[];  // plane k at q4 + k * HWs; geometry after
-    __shared__ int s_red[4 * (NT / 64)];
+    __shared__ int s_red[2 * (NT / 64)];
     __shared__ int s_next;
+    const int b = blockIdx.z;
+    const int c0 = blockIdx.x * CG;
     const int tid = threadIdx.x, lane = tid & 63;
     const int HW = H * W;
     const int HWs = (HW + 15) & ~15;
     const int PHW = PH * PW;
-    const int G = static_cast<int>(gridDim.x);
-    const int gi = static_cast<int>(blockIdx.x);
-    const int gr = (G & 7) == 0 ? (gi & 7) * (G >> 3) + (gi >> 3) : gi;  // XCD-major renumbering
-    const int U = (C / CG) * R;  // < 2^31 (px_plan)
-    const int u_lo = static_cast<int>(static_cast<int64_t>(U) * gr / G);
-    const int u_hi = static_cast<int>(static_cast<int64_t>(U) * (gr + 1) / G);
-    if (u_lo >= u_hi) return;
-    const float* bsrc = HEAD ? hd.inds : rois;  // batch index of RoI r at bsrc[r * bstr]
-    const int bstr = HEAD ? 1 : 5;
+    const int split = gridDim.y, z = blockIdx.y;
+    const int N = gridDim.z - 1;
+    if (b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
+        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, 0, N, s_red, 1)
+                             : roi_range_sorted<NT>(rois, R, 0, N, s_red);
+        const int n_lo = rg.x, tot = n_lo + (R - rg.y);
+        const int lo = static_cast<int>(static_cast<int64_t>(tot) * z / split);
+        const int hi = static_cast<int>(static_cast<int64_t>(tot) * (z + 1) / split);
+        if (HEAD && hd.boxes && blockIdx.x == 0)
+            for (int t = lo + tid; t < hi; t += NT) {
+                const int r = t < n_lo ? t : rg.y + (t - n_lo);
+                float bx[5];
+                head_box(rois, hd, r, bx);
+#pragma unroll
+                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
+            }
+        for (int e = lo * CG * PHW + tid; e < hi * CG * PHW; e += NT) {
+            const int t = e / (CG * PHW);
+            const int rem = e - t * (CG * PHW);
+            const int r = t < n_lo ? t : rg.y + (t - n_lo);
+            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + rem;
+            out[o] = 0.0f;
+            argmax[o] = -1;
+        }
+        return;
+    }
+    const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, b, b + 1, s_red, 1)
+                         : roi_range_sorted<NT>(rois, R, b, b + 1, s_red);
+    const int rbase = rg.x, nr = rg.y - rg.x;
+    if (z >= nr) return;
+    const int nmine = (nr - z + split - 1) / split;  // items z, z+split, ...
+    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+    for (int p = tid; p < HW; p += NT) {
+        float v[CG];
+#pragma unroll
+        for (int q = 0; q < CG; ++q) {
+            const float e = src[static_cast<size_t>(q) * HW + p];
+            v[q] = e;
+        }
+        const float4* pp = tile_px<NP>(q4, p);
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            const_cast<float4*>(pp)[16 * k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    }
     int4* s_geo = reinterpret_cast<int4*>(q4 + NP * HWs);
-    int* s_rid = reinterpret_cast<int*>(s_geo + geo_cap);
     const int ph = lane / PW, pw = lane - (lane / PW) * PW;
     const bool act = lane < PHW;
-    // CG channel planes of image b from channel c0 into LDS (tile_px layout)
-    auto stage = [&](int b, int c0) {
-        const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
-        for (int p = tid; p < HW; p += NT) {
-            float v[CG];
+    for (int k0 = 0; k0 < nmine; k0 += geo_cap) {
+        const int cn = min(geo_cap, nmine - k0);
+        for (int i = tid; i < cn; i += NT) {
+            const int r = rbase + z + (k0 + i) * split;
+            float bx[5];
+            if (HEAD) {
+                head_box(rois, hd, r, bx);
+                if (hd.boxes && blockIdx.x == 0) {
 #pragma unroll
-            for (int q = 0; q < CG; ++q) v[q] = src[static_cast<size_t>(q) * HW + p];
-            const float4* pp = tile_px<NP>(q4, p);
-#pragma unroll
-            for (int k = 0; k < NP; ++k)
-                const_cast<float4*>(pp)[16 * k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
-        }
-    };
-    // The first segment's planes are staged before the RoI-range pass (its loads
-    // overlap the staging's); a batch index outside [0, N) stages nothing.
-    const int cg_first = u_lo / R;
-    const int b_first = static_cast<int>(bsrc[static_cast<size_t>(u_lo - cg_first * R) * bstr]);
-    const bool first_ok = b_first >= 0 && b_first < N;
-    if (first_ok) stage(b_first, cg_first * CG);
-    // one pass: RoIs with batch index in [0, N), and the range of the first unit's image
-    const int4 cnt4 = roi_counts4<NT>(bsrc, R, make_int4(0, N, b_first, b_first + 1), s_red, bstr);
-    const int2 vr = make_int2(cnt4.x, cnt4.y);
-    bool staged = first_ok;
-    for (int u = u_lo; u < u_hi;) {
-        const int cgi = u / R;
-        const int j = u - cgi * R;
-        const int c0 = cgi * CG;
-        int b = -1, j_beg = 0, j_end;
-        if (j < vr.x || j >= vr.y) {
-            j_end = j < vr.x ? vr.x : R;
-        } else {
-            b = static_cast<int>(bsrc[static_cast<size_t>(j) * bstr]);
-            const int2 ir = b == b_first ? make_int2(cnt4.z, cnt4.w)
-                                         : roi_range_sorted<NT>(bsrc, R, b, b + 1, s_red, bstr);
-            j_beg = ir.x;
-            j_end = ir.y;
-        }
-        const int seg_hi = min(u_hi, cgi * R + j_end);
-        const int n = seg_hi - u;  // RoIs j .. j + n - 1
-        u = seg_hi;
-        if (b < 0) {  // out-of-range batch index: torchvision reads out of bounds; we write 0 / -1
-            if (HEAD && hd.boxes && cgi == 0)
-                for (int t = tid; t < n; t += NT) {
-                    float bx[5];
-                    head_box(rois, hd, j + t, bx);
-#pragma unroll
-                    for (int q = 0; q < 5; ++q) hd.boxes[static_cast<size_t>(j + t) * 5 + q] = bx[q];
+                    for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
                 }
-            for (int e = tid; e < n * CG * PHW; e += NT) {
-                const int t = e / (CG * PHW);
-                const size_t o = (static_cast<size_t>(j + t) * C + c0) * PHW + (e - t * (CG * PHW));
-                out[o] = 0.0f;
-                argmax[o] = -1;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 5; ++j) bx[j] = rois[static_cast<size_t>(r) * 5 + j];
             }
-            continue;
+            const RoiGeom gm = roi_geom(bx, ss, PH, PW);
+            s_geo[i] = make_int4(gm.sh, gm.sw, __float_as_int(gm.bh), __float_as_int(gm.bw));
         }
-        // The image's n RoIs in column order of an L x S grid (RoI = row * S + col):
-        // S ~ the number of workgroups sharing the image, so a workgroup's unit
-        // range is about one column -- RoIs col, col + S, ... -- which samples the
-        // whole score order (RoI cost varies 100x) and is walked in score order.
-        const int nimg = j_end - j_beg;
-        const int per_wg = (U + G - 1) / G;
-        const int S = max(1, min(nimg, (nimg + per_wg / 2) / per_wg));
-        const int L = (nimg + S - 1) / S;
-        const int F = nimg - (L - 1) * S;  // columns with L RoIs (the rest have L - 1)
-        const int kbase = j - j_beg;
-        if (!staged) stage(b, c0);
-        staged = false;  // a later segment is another (channel group, image)
-        for (int k0 = 0; k0 < n; k0 += geo_cap) {
-            const int cn = min(geo_cap, n - k0);
-            for (int i = tid; i < cn; i += NT) {
-                const int kk = kbase + k0 + i;
-                const int col = kk < F * L ? kk / L : F + (kk - F * L) / max(L - 1, 1);
-                const int row = kk < F * L ? kk - col * L : (kk - F * L) - (col - F) * (L - 1);
-                const int r = j_beg + row * S + col;
-                s_rid[i] = r;
-                float bx[5];
-                if (HEAD) {
-                    head_box(rois, hd, r, bx);
-                    if (hd.boxes && cgi == 0) {
+        if (tid == 0) s_next = 0;
+        __syncthreads();
+        int k = 0;
+        if (lane == 0) k = atomicAdd(&s_next, 1);
+        k = __builtin_amdgcn_readfirstlane(k);
+        while (k < cn) {
+            int kn = 0;
+            if (lane == 0) kn = atomicAdd(&s_next, 1);  // prefetch the next item
+            const int r = rbase + z + (k0 + k) * split;
+            const int4 gq = s_geo[k];
+            RoiGeom gm;
+            gm.sh = gq.x;
+            gm.sw = gq.y;
+            gm.bh = __int_as_float(gq.z);
+            gm.bw = __int_as_float(gq.w);
+            int4 g = geom_bin(gm, H, W, ph, pw);
+            if (!act) g = make_int4(0, 0, 0, 0);
+            const bool empty = g.y <= g.x || g.w <= g.z;
+            float mv[CG];
+            int mi[CG];
 #pragma unroll
-                        for (int q = 0; q < 5; ++q) hd.boxes[static_cast<size_t>(r) * 5 + q] = bx[q];
-                    }
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 5; ++q) bx[q] = rois[static_cast<size_t>(r) * 5 + q];
-                }
-                const RoiGeom gm = roi_geom(bx, ss, PH, PW);
-                s_geo[i] = make_int4(gm.sh, gm.sw, __float_as_int(gm.bh), __float_as_int(gm.bw));
+            for (int c = 0; c < CG; ++c) {
+                mv[c] = empty ? 0.0f : -FLT_MAX;
+                mi[c] = -1;
             }
-            if (tid == 0) s_next = 0;
-            __syncthreads();  // tile + geometry visible
-            int k = 0;
-            if (lane == 0) k = atomicAdd(&s_next, 1);
-            k = __builtin_amdgcn_readfirstlane(k);
-            while (k < cn) {
-                int kn = 0;
-                if (lane == 0) kn = atomicAdd(&s_next, 1);  // prefetch the next item
-                const int r = s_rid[k];
-                const int4 gq = s_geo[k];
-                RoiGeom gm;
-                gm.sh = gq.x;
-                gm.sw = gq.y;
-                gm.bh = __int_as_float(gq.z);
-                gm.bw = __int_as_float(gq.w);
-                int4 g = geom_bin(gm, H, W, ph, pw);
-                if (!act) g = make_int4(0, 0, 0, 0);
-                const bool empty = g.y <= g.x || g.w <= g.z;
-                float mv[CG];
-                int mi[CG];
+            for (int h = g.x; h < g.y; ++h) {
+                const int rb = h * W;
+                for (int w = g.z; w < g.w; ++w) {
+                    const int ii = rb + w;
+                    const float4* pp = tile_px<NP>(q4, ii);
+                    float4 v[NP];
 #pragma unroll
-                for (int c = 0; c < CG; ++c) {
-                    mv[c] = empty ? 0.0f : -FLT_MAX;
-                    mi[c] = -1;
-                }
-                const char* tb = reinterpret_cast<const char*>(q4);
-                for (int h = g.x; h < g.y; ++h) {
-                    const int r16 = h * W * 16;
-                    // p16 = 16 * pixel index: the loop counter, the LDS offset's source and
-                    // (scaled) the argmax, so a pixel step costs 5 VALU besides the compares
-                    for (int p16 = r16 + g.z * 16; p16 < r16 + g.w * 16; p16 += 16) {
-                        const float4* pp = reinterpret_cast<const float4*>(tb + tile_off16<NP>(p16));
-                        float4 v[NP];
+                    for (int q = 0; q < NP; ++q) v[q] = pp[16 * q];
+                    // all NP reads in flight before the first compare (else the compiler
+                    // waits on each read in turn: NP LDS round trips per pixel)
+                    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                        for (int q = 0; q < NP; ++q) v[q] = pp[16 * q];
-                        // all NP reads in flight before the first compare (else the compiler
-                        // waits on each read in turn: NP LDS round trips per pixel)
-                        __builtin_amdgcn_sched_barrier(0);
+                    for (int q = 0; q < NP; ++q) {
+                        const float vv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
-                        for (int q = 0; q < NP; ++q) {
-                            const float vv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
-#pragma unroll
-                            for (int jj = 0; jj < 4; ++jj) {
-                                if (vv[jj] > mv[4 * q + jj]) {  // torchvision's strict '>'
-                                    mv[4 * q + jj] = vv[jj];
-                                    mi[4 * q + jj] = p16;
-                                }
+                        for (int j = 0; j < 4; ++j) {
+                            if (vv[j] > mv[4 * q + j]) {  // torchvision's strict '>'
+                                mv[4 * q + j] = vv[j];
+                                mi[4 * q + j] = ii;
                             }
                         }
                     }
                 }
-                if (act) {
-                    const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
-#pragma unroll
-                    for (int c = 0; c < CG; ++c) {
-                        out[o + static_cast<size_t>(c) * PHW] = mv[c];
-                        argmax[o + static_cast<size_t>(c) * PHW] = mi[c] >> 4;  // -1 stays -1
-                    }
-                }
-                k = __builtin_amdgcn_readfirstlane(kn);
             }
-            __syncthreads();  // the chunk's geometry, s_next and (after the last chunk) the tile are reused
+            if (act) {
+                const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
+#pragma unroll
+                for (int c = 0; c < CG; ++c) {
+                    out[o + static_cast<size_t>(c) * PHW] = mv[c];
+                    argmax[o + static_cast<size_t>(c) * PHW] = mi[c];
+                }
+            }
+            k = __builtin_amdgcn_readfirstlane(kn);
         }
+        __syncthreads();  // the chunk's geometry and s_next are reused
     }
 }
 
@@ -1152,19 +1070,19 @@ FwdWs carve_fwd(void* ws, int64_t R, int N) {
 
 // Launch plan of the wave-per-RoI forward: CG = 16 channel planes when they
 // fit the CU's LDS (one workgroup per CU), else 8 (two per CU when they fit),
-// else 4.  Each workgroup gets the LDS left over for its RoI-geometry chunk.
-// Grid = one workgroup per resident slot of the CUs the launch stream may use
-// (roi_pool_split > 0 overrides: split x images x channel groups).
+// else 4.  Each workgroup gets the LDS left over for its RoI-geometry chunk;
+// split = RoI shares per (image, channel group), sized so the grid fills every
+// resident slot of the CUs the launch stream may use once.
 struct PxPlan {
-    int cg = 0, geo_cap = 0, grid = 0;
+    int cg = 0, geo_cap = 0, split = 1;
     size_t lds = 0;
 };
-PxPlan px_plan(int C, int N, int H, int W, int PHW, int64_t R, hipStream_t st) {
+PxPlan px_plan(int C, int N, int H, int W, int PHW, hipStream_t st) {
     PxPlan pl;
     const size_t HW = static_cast<size_t>(H) * W;
     if (N <= 0 || HW == 0 || PHW > 64 || H > 65535 || W > 65535) return pl;
     constexpr size_t kReserve = 1024;  // static LDS + allocation rounding
-    constexpr size_t kMinGeo = 64 * (sizeof(int4) + sizeof(int));
+    constexpr size_t kMinGeo = 64 * sizeof(int4);
     const size_t HWs = (HW + 15) & ~static_cast<size_t>(15);
     for (int cg : {16, 8, 4}) {
         if (C % cg != 0) continue;
@@ -1174,16 +1092,14 @@ PxPlan px_plan(int C, int N, int H, int W, int PHW, int64_t R, hipStream_t st) {
         if (2 * (tile + kMinGeo + kReserve) <= kLdsPerCu) per_cu = 2;
         else if (tile + kMinGeo + kReserve <= kLdsPerCu) per_cu = 1;
         if (!per_cu) continue;
-        const size_t geo = (kLdsPerCu / per_cu - kReserve - tile) / (sizeof(int4) + sizeof(int));
+        const size_t geo = (kLdsPerCu / per_cu - kReserve - tile) / sizeof(int4);
         pl.geo_cap = static_cast<int>(geo > 512 ? 512 : geo);
         pl.cg = cg;
-        pl.lds = tile + static_cast<size_t>(pl.geo_cap) * (sizeof(int4) + sizeof(int));
-        if (static_cast<int64_t>(C / cg) * R >= (int64_t{1} << 31)) return PxPlan{};  // unit index is 32-bit
-        int64_t g = static_cast<int64_t>(stream_cu_count(st)) * per_cu;
-        if (path_cfg().roi_split > 0)  // A/B override
-            g = static_cast<int64_t>(path_cfg().roi_split) * (C / cg) * N;
-        if (path_cfg().roi_wgs > 0) g = path_cfg().roi_wgs;  // caller leaves CUs to concurrent work
-        pl.grid = static_cast<int>(g < 1 ? 1 : (g > 65535 ? 65535 : g));
+        pl.lds = tile + static_cast<size_t>(pl.geo_cap) * sizeof(int4);
+        const int64_t wgs = static_cast<int64_t>(C / cg) * N;
+        int64_t sp = (static_cast<int64_t>(stream_cu_count(st)) * per_cu + wgs - 1) / wgs;
+        if (path_cfg().roi_split > 0) sp = path_cfg().roi_split;  // A/B override
+        pl.split = static_cast<int>(sp < 1 ? 1 : (sp > 64 ? 64 : sp));
         return pl;
     }
     return pl;
@@ -1192,10 +1108,10 @@ PxPlan px_plan(int C, int N, int H, int W, int PHW, int64_t R, hipStream_t st) {
 template <bool HEAD>
 int px_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
               int PH, int PW, float ss, float* out, int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
-    const dim3 grid(static_cast<unsigned>(pl.grid));
+    const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(pl.split), static_cast<unsigned>(N + 1));
 #define FRCNN_PX(CG)                                                                                    \
     hipLaunchKernelGGL((roi_pool_fwd_wave_kernel<1024, CG, HEAD>), grid, dim3(1024), pl.lds, st, x, rois, \
-                       static_cast<int>(R), N, C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd)
+                       static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd)
     if (pl.cg == 16) FRCNN_PX(16);
     else if (pl.cg == 8) FRCNN_PX(8);
     else FRCNN_PX(4);
@@ -1246,8 +1162,8 @@ template <bool HEAD, bool LIST>
 int dense_launch(const DensePlan& pl, const float* x, const float* rois, const int* list, const int* cnt,
                  int64_t R, int N, int C, int H, int W, int PH, int PW, float ss, float* out,
                  int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
-    const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(LIST ? N : N + 1),
-                    static_cast<unsigned>(pl.split));
+    const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(pl.split),
+                    static_cast<unsigned>(LIST ? N : N + 1));
     const bool fix7 = PH == 7 && PW == 7;
 #define FRCNN_DENSE(CG, FX)                                                                               \
     hipLaunchKernelGGL((roi_pool_fwd_dense_kernel<1024, CG, FX, HEAD, LIST>), grid, dim3(1024), pl.lds, st, \
@@ -1283,7 +1199,7 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
     FRCNN_REQUIRE(x && rois && out && argmax, "frcnn_roi_pool_fwd: null pointer");
     hipStream_t st = as_stream(stream);
     const int path = path_cfg().roi_fwd;
-    const PxPlan xp = (rois_sorted && (path == kPathAuto || path == kPathWave)) ? px_plan(C, N, H, W, PH * PW, R, st)
+    const PxPlan xp = (rois_sorted && (path == kPathAuto || path == kPathWave)) ? px_plan(C, N, H, W, PH * PW, st)
                                                                               : PxPlan{};
     if (xp.cg)
         return px_launch<false>(xp, x, rois, R, N, C, H, W, PH, PW, spatial_scale, out, argmax, HeadArgs{}, st);
@@ -1334,7 +1250,7 @@ extern "C" int frcnn_roi_pool_fwd_head(const float* x, const float* rois, const 
     const int path = path_cfg().roi_fwd;
     const bool aligned = reinterpret_cast<uintptr_t>(rois) % 16 == 0;
     const PxPlan xp = (rois_sorted && C > 0 && aligned && (path == kPathAuto || path == kPathWave))
-                          ? px_plan(C, N, H, W, PH * PW, R, as_stream(stream))
+                          ? px_plan(C, N, H, W, PH * PW, as_stream(stream))
                           : PxPlan{};
     if (xp.cg) {  // transform + pack inside the pool kernel
         FRCNN_REQUIRE(x && out && argmax, "frcnn_roi_pool_fwd_head: null pointer");
