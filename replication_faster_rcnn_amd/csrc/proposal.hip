@@ -212,9 +212,11 @@ __global__ __launch_bounds__(1024) void merge_rank_kernel(const uint64_t* __rest
 
 // Per-image state of the staged NMS (carried from one stage launch to the next).
 struct SweepState {
-    int* count;      // [N] boxes kept so far
-    int* done;       // [N] post_nms reached or every candidate examined
-    uint64_t* kept;  // [N][Wc] kept bits of each 64-candidate block
+    int* count;        // [N] boxes kept so far
+    int* done;         // [N] post_nms reached or every candidate examined
+    uint64_t* kept;    // [N][Wc] kept bits of each 64-candidate block
+    uint64_t* prehit;  // [N][Wc] columns hit by a box kept in an earlier stage
+    int wc;
 };
 
 __global__ __launch_bounds__(1024) void rank_scatter_kernel(const uint64_t* __restrict__ runs_all,
@@ -233,6 +235,8 @@ __global__ __launch_bounds__(1024) void rank_scatter_kernel(const uint64_t* __re
         ss.count[n] = 0;
         ss.done[n] = 0;
     }
+    if (i == 0)
+        for (int b = tid; b < ss.wc; b += 1024) ss.prehit[static_cast<size_t>(n) * ss.wc + b] = 0ull;
     const int len = min(kRun, A - i * kRun);
     if (tid >= len) return;
     const uint64_t key = runs_all[static_cast<size_t>(n) * nr * kRun + i * kRun + tid];
@@ -291,7 +295,9 @@ __global__ __launch_bounds__(256) void nms_mask_stage_kernel(const float4* __res
                                                              int Wc, const int* __restrict__ sel_P,
                                                              const int* __restrict__ done, int cb0,
                                                              int ntiles, NmsThr thr,
-                                                             uint64_t* __restrict__ maskC) {
+                                                             uint64_t* __restrict__ maskC,
+                                                             const uint64_t* __restrict__ kept_all,
+                                                             uint64_t* __restrict__ prehit) {
     const int n = blockIdx.y;
     if (done[n]) return;
     const int P = sel_P[n];
@@ -306,6 +312,11 @@ __global__ __launch_bounds__(256) void nms_mask_stage_kernel(const float4* __res
         stage_tile(t, cb0, rb, cb);
         if (cb >= nbP) break;  // tiles go by column: the rest are past the candidates too
         if (rb >= nbP) continue;
+        // Rows of earlier stages are settled: only their kept rows matter, and only
+        // as "is the column hit" -- one bit per column, OR-ed into prehit.
+        const bool settled = rb < cb0;
+        const uint64_t K = settled ? kept_all[static_cast<size_t>(n) * Wc + rb] : ~0ull;
+        if (K == 0ull) continue;  // uniform
         const int i0 = rb * 64;
         __syncthreads();  // the previous tile is done with rbox / part
         if (tid < 64 && i0 + tid < P) {
@@ -326,20 +337,30 @@ __global__ __launch_bounds__(256) void nms_mask_stage_kernel(const float4* __res
             const int r0 = wid * 16;
 #pragma unroll 4
             for (int ii = r0; ii < r0 + 16; ++ii)
-                if (ii < iend && iou_over(rbox[ii], rarea[ii], bj, aj, thr)) bits |= 1ull << ii;
+                if (ii < iend && ((K >> ii) & 1ull) && iou_over(rbox[ii], rarea[ii], bj, aj, thr))
+                    bits |= 1ull << ii;
         }
         part[wid][lane] = bits;
         __syncthreads();
-        if (wid == 0 && jv)
-            maskC[((static_cast<size_t>(n) * Wc + cb) * Wc + rb) * 64 + lane] =
-                part[0][lane] | part[1][lane] | part[2][lane] | part[3][lane];
+        if (wid == 0) {
+            const uint64_t word = part[0][lane] | part[1][lane] | part[2][lane] | part[3][lane];
+            if (settled) {
+                const uint64_t h = __ballot(jv && word != 0ull);
+                if (lane == 0 && h) atomicOr(reinterpret_cast<unsigned long long*>(prehit) +
+                                                 static_cast<size_t>(n) * Wc + cb,
+                                             static_cast<unsigned long long>(h));
+            } else if (jv) {
+                maskC[((static_cast<size_t>(n) * Wc + cb) * Wc + rb) * 64 + lane] = word;
+            }
+        }
     }
 }
 
 // One 1024-thread workgroup per image continues the greedy sweep over the
 // stage's blocks [cb0, cb1), 16 blocks (1024 candidates) at a time: wave w owns
-// column block sb0 + w, lane = column.  Each lane first ORs in the kept rows of
-// every earlier block (one round of independent loads), then holds the
+// column block sb0 + w, lane = column.  Each lane starts from its prehit bit
+// (hit by a box kept in an earlier stage, from the mask kernel), ORs in the
+// kept rows of the stage's earlier blocks (one round of independent loads), then holds the
 // column-form words of the sub-stage's earlier blocks in registers, so the
 // sub-stage resolves block after block with one barrier each and no memory
 // latency: wave q computes avail = ~hit, runs the fixed point
@@ -369,8 +390,7 @@ __global__ __launch_bounds__(1024) void nms_sweep_stage_kernel(
     const int32_t* sidx = sidx_all + static_cast<size_t>(n) * pre;
     uint64_t* gkept = ss.kept + static_cast<size_t>(n) * Wc;
     int count = ss.count[n];
-    for (int b = tid; b < cb0; b += 1024) kept[b] = gkept[b];
-    __syncthreads();
+    // rows of earlier stages reach this stage only through ss.prehit
     for (int sb0 = cb0; sb0 < end && count < post; sb0 += kSub) {
         const int nsb = min(kSub, end - sb0);
         const int cb = sb0 + wid;  // this wave's column block
@@ -386,7 +406,8 @@ __global__ __launch_bounds__(1024) void nms_sweep_stage_kernel(
             sj = sidx[j];
         }
         if (mine) {
-            for (int rb = 0; rb < sb0; ++rb) hit |= (colw[static_cast<size_t>(rb) * 64] & kept[rb]) != 0ull;
+            hit = ((ss.prehit[static_cast<size_t>(n) * Wc + cb] >> lane) & 1ull) != 0ull;  // earlier stages
+            for (int rb = cb0; rb < sb0; ++rb) hit |= (colw[static_cast<size_t>(rb) * 64] & kept[rb]) != 0ull;
 #pragma unroll
             for (int q = 0; q < kSub; ++q) col[q] = q <= wid ? colw[static_cast<size_t>(sb0 + q) * 64] : 0ull;
         }
@@ -950,6 +971,8 @@ static ProposeWs carve(void* ws, int N, int A, int pre, bool need_boxes) {
     w.ss.count = c.take<int>(N);
     w.ss.done = c.take<int>(N);
     w.ss.kept = c.take<uint64_t>(static_cast<size_t>(N) * Wc);
+    w.ss.prehit = c.take<uint64_t>(static_cast<size_t>(N) * Wc);
+    w.ss.wc = Wc;
     w.hyb.cbox = c.take<float4>(static_cast<size_t>(N) * kChunk);
     w.hyb.ckey = c.take<uint64_t>(static_cast<size_t>(N) * kChunk);
     w.hyb.cc = c.take<int>(N);
@@ -984,7 +1007,7 @@ static int sort_and_suppress(const ProposeWs& w, const float4* box_src, int N, i
         const int64_t tiles = static_cast<int64_t>(cb1) * (cb1 + 1) / 2 - static_cast<int64_t>(cb0) * (cb0 + 1) / 2;
         const unsigned grid = static_cast<unsigned>(tiles < kMaskGrid ? tiles : kMaskGrid);
         hipLaunchKernelGGL(nms_mask_stage_kernel, dim3(grid, N), dim3(256), 0, st, w.sbox, pre, Wc, w.sel_P,
-                           w.ss.done, cb0, static_cast<int>(tiles), thr, w.maskC);
+                           w.ss.done, cb0, static_cast<int>(tiles), thr, w.maskC, w.ss.kept, w.ss.prehit);
         FRCNN_LAUNCH_CHECK("nms_mask_stage_kernel");
         const size_t lds = static_cast<size_t>(Wc) * sizeof(uint64_t);
         if (out_mode == 0)
