@@ -416,10 +416,13 @@ def train_step_fn(args, c, sc, de, x, base, first_image, ev):
     RoI transform + pack + RoIPool forward -> RoIPool backward of a resident
     upstream gradient (the head's dL/dpool).
 
-    With --streams 2 the step runs on three HIP streams: the target creators
-    (the device RNG stream: AT(k), PT(k), AT(k+1), ... in the reference's order)
-    on one, the proposal layer on another -- AT(k) needs only the gt boxes and
-    the anchors, so it starts before step k's proposals are done -- and the
+    With --streams 2 the step runs on three HIP streams (HIP multiplexes streams
+    onto 4 hardware queues, one of them torch's default stream, so a fourth
+    stream would share a queue): the target creators' draws (the device RNG
+    stream: AT(k), PT(k), AT(k+1), ... in the reference's order) on one;
+    AnchorTargetCreator's RNG-free half (IoU, labels, candidate lists) and then
+    the proposal layer on another -- AT(k) needs only the gt boxes and the
+    anchors, so its draws start before step k's proposals are done -- and the
     RoIPool forward + backward of step k on a third, beside AT(k+1)."""
     from replication_faster_rcnn_amd import anchors as A, ops, synth, targets
     from replication_faster_rcnn_amd.utils import rng_state_to_device
@@ -437,11 +440,30 @@ def train_step_fn(args, c, sc, de, x, base, first_image, ev):
     grad = torch.randn((N * S, x.size(1), 7, 7), device=dev, generator=gen)
     if args.streams == 1:
         s_prop = s_rng = s_pool = torch.cuda.current_stream()
-    else:
+    else:  # three streams: HIP maps streams onto 4 hardware queues (one is torch's default)
         s_prop, s_rng, s_pool = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    s_prep = s_prop
     state = {}
+    # AnchorTargetCreator's RNG-free half (IoU, labels, candidate lists) of step
+    # k runs on the proposal stream, ahead of step k's proposals and beside step
+    # k-1's draws; two workspaces alternate
+    A_ = anchors.size(0)
+    at_ws = [targets.anchor_targets_workspace(N, A_, boxes.size(1), dev) for _ in range(2)]
+    at_out = [(torch.empty((N, A_, 4), dtype=torch.float64, device=dev),
+               torch.empty((N, A_), dtype=torch.int32, device=dev)) for _ in range(2)]
+    prep_ready = [torch.cuda.Event() for _ in range(2)]
+    sample_done = [None, None]
+    sample_ev = [torch.cuda.Event() for _ in range(2)]
+    k_step = [0]
 
     def step(timed):
+        j = k_step[0] % 2
+        k_step[0] += 1
+        with torch.cuda.stream(s_prep):
+            if sample_done[j] is not None:
+                s_prep.wait_event(sample_done[j])  # the draws that read at_ws[j] last time
+            plan = targets.anchor_targets_prepare(boxes, labels, anchors, workspace=at_ws[j])
+            prep_ready[j].record(s_prep)
         with torch.cuda.stream(s_prop):
             rois, _, cnt = ops.propose(sc, de, img_w=c["img_w"], img_h=c["img_h"],
                                        pre_nms=c["pre_nms"], post_nms=c["post_nms"],
@@ -449,7 +471,10 @@ def train_step_fn(args, c, sc, de, x, base, first_image, ev):
             prop_ready = torch.cuda.Event()
             prop_ready.record(s_prop)
         with torch.cuda.stream(s_rng):
-            reg_t, lab = targets.anchor_targets(boxes, labels, anchors, rng=rng)
+            s_rng.wait_event(prep_ready[j])
+            reg_t, lab = targets.anchor_targets_sample(plan, rng=rng, out=at_out[j])
+            sample_ev[j].record(s_rng)
+            sample_done[j] = sample_ev[j]
             s_rng.wait_event(prop_ready)
             rois.record_stream(s_rng)   # allocated on s_prop, read on s_rng
             cnt.record_stream(s_rng)

@@ -208,6 +208,22 @@ int frcnn_anchor_target(int N, int A, int G, const float* anchors, const double*
                         double* reg, int32_t* label, int32_t* argmax, double* max_iou,
                         void* workspace, size_t ws_bytes, void* stream);
 
+/* frcnn_anchor_target in two halves on one workspace (frcnn_anchor_target =
+ * prepare + sample on the same stream):
+ *   prepare: gt compaction, anchor x gt IoU, labels and the ordered positive /
+ *            negative lists (utils/utils.py:146-188) -- no RNG, so a training
+ *            loop can run it ahead, on another stream, beside the previous
+ *            step's draws;
+ *   sample:  the np.random.choice draws on rng_state (utils/utils.py:190-202)
+ *            and the regression targets; runs after prepare on the same
+ *            workspace (order the streams with an event). */
+int frcnn_anchor_target_prepare(int N, int A, int G, const float* anchors, const double* boxes,
+                                const double* labels, double pos_iou_thresh, double neg_iou_thresh,
+                                void* workspace, size_t ws_bytes, void* stream);
+int frcnn_anchor_target_sample(int N, int A, int G, const float* anchors, int n_sample, double pos_ratio,
+                               uint32_t* rng_state, double* reg, int32_t* label, int32_t* argmax,
+                               double* max_iou, void* workspace, size_t ws_bytes, void* stream);
+
 /* utils/utils.py:207-276 ProposalTargetCreator.__call__, batched over N images in
  * the order of train.py:91-104.
  *   rois fp32 [N,Rp,4] with rcount int32 [N] valid rows per image; boxes/labels as

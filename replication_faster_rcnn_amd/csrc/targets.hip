@@ -952,21 +952,17 @@ extern "C" size_t frcnn_anchor_target_workspace_size(int N, int A, int G) {
     return carve_at(nullptr, N, A, G > 0 ? G : 1).bytes;
 }
 
-extern "C" int frcnn_anchor_target(int N, int A, int G, const float* anchors, const double* boxes,
-                                   const double* labels, int n_sample, double pos_iou_thresh,
-                                   double neg_iou_thresh, double pos_ratio, uint32_t* rng_state,
-                                   double* reg, int32_t* label, int32_t* argmax, double* max_iou,
-                                   void* workspace, size_t ws_bytes, void* stream) {
+extern "C" int frcnn_anchor_target_prepare(int N, int A, int G, const float* anchors, const double* boxes,
+                                           const double* labels, double pos_iou_thresh,
+                                           double neg_iou_thresh, void* workspace, size_t ws_bytes,
+                                           void* stream) {
     FRCNN_REQUIRE(N > 0 && N <= 65535 && A > 0 && G >= 0 && G <= kMaxG,
-                  "frcnn_anchor_target: need 0 < N <= 65535, A > 0, 0 <= G <= %d", kMaxG);
-    FRCNN_REQUIRE(anchors && reg && label, "frcnn_anchor_target: null pointer");
-    FRCNN_REQUIRE(G == 0 || (boxes && labels), "frcnn_anchor_target: null boxes");
-    const int n_pos_max = static_cast<int>(pos_ratio * n_sample);  // int(0.5*256) (utils/utils.py:190)
-    FRCNN_REQUIRE(n_sample - (n_pos_max < 0 ? 0 : n_pos_max) <= kMaxKeep && n_pos_max <= kMaxKeep,
-                  "frcnn_anchor_target: n_sample too large");
+                  "frcnn_anchor_target_prepare: need 0 < N <= 65535, A > 0, 0 <= G <= %d", kMaxG);
+    FRCNN_REQUIRE(anchors, "frcnn_anchor_target_prepare: null anchors");
+    FRCNN_REQUIRE(G == 0 || (boxes && labels), "frcnn_anchor_target_prepare: null boxes");
     const int Gp = G > 0 ? G : 1;
     AtWs w = carve_at(workspace, N, A, Gp);
-    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_anchor_target: workspace %zu < %zu",
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_anchor_target_prepare: workspace %zu < %zu",
                   ws_bytes, w.bytes);
     hipStream_t st = as_stream(stream);
     if (G > 0) {
@@ -974,7 +970,7 @@ extern "C" int frcnn_anchor_target(int N, int A, int G, const float* anchors, co
                            w.gcount);
         FRCNN_LAUNCH_CHECK("gt_compact_kernel");
     } else if (hipMemsetAsync(w.gcount, 0, sizeof(int) * N, st) != hipSuccess) {
-        return check_launch("frcnn_anchor_target memset");
+        return check_launch("frcnn_anchor_target_prepare memset");
     }
     const int nblk = (A + 255) / 256;
     hipLaunchKernelGGL(at_iou_kernel, dim3(nblk, N), dim3(256), 0, st, anchors, A, w.gt, w.gcount,
@@ -985,24 +981,59 @@ extern "C" int frcnn_anchor_target(int N, int A, int G, const float* anchors, co
                        w.label0, w.pos_list, w.neg_list, w.npos, w.nneg);
     FRCNN_LAUNCH_CHECK("at_label_kernel");
     if (hipMemsetAsync(w.keep, 0, static_cast<size_t>(N) * A, st) != hipSuccess)
-        return check_launch("frcnn_anchor_target memset");
+        return check_launch("frcnn_anchor_target_prepare memset");
+    return FRCNN_OK;
+}
+
+extern "C" int frcnn_anchor_target_sample(int N, int A, int G, const float* anchors, int n_sample,
+                                          double pos_ratio, uint32_t* rng_state, double* reg,
+                                          int32_t* label, int32_t* argmax, double* max_iou,
+                                          void* workspace, size_t ws_bytes, void* stream) {
+    FRCNN_REQUIRE(N > 0 && N <= 65535 && A > 0 && G >= 0 && G <= kMaxG,
+                  "frcnn_anchor_target_sample: need 0 < N <= 65535, A > 0, 0 <= G <= %d", kMaxG);
+    FRCNN_REQUIRE(anchors && reg && label, "frcnn_anchor_target_sample: null pointer");
+    const int n_pos_max = static_cast<int>(pos_ratio * n_sample);  // int(0.5*256) (utils/utils.py:190)
+    FRCNN_REQUIRE(n_sample - (n_pos_max < 0 ? 0 : n_pos_max) <= kMaxKeep && n_pos_max <= kMaxKeep,
+                  "frcnn_anchor_target_sample: n_sample too large");
+    const int Gp = G > 0 ? G : 1;
+    AtWs w = carve_at(workspace, N, A, Gp);
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_anchor_target_sample: workspace %zu < %zu",
+                  ws_bytes, w.bytes);
+    hipStream_t st = as_stream(stream);
+    const int nblk = (A + 255) / 256;
     if (rng_state) {
         hipLaunchKernelGGL(at_sample_kernel, dim3(1), dim3(kSampThreads), 0, st, N, A, n_sample, n_pos_max,
                            w.pos_list, w.neg_list, w.npos, w.nneg, rng_state, w.keep, w.sampled);
         FRCNN_LAUNCH_CHECK("at_sample_kernel");
     } else if (hipMemsetAsync(w.sampled, 0, sizeof(int) * 2 * N, st) != hipSuccess) {
-        return check_launch("frcnn_anchor_target memset");
+        return check_launch("frcnn_anchor_target_sample memset");
     }
     hipLaunchKernelGGL(at_finish_kernel, dim3(nblk, N), dim3(256), 0, st, anchors, A, w.gt, w.gcount,
                        Gp, w.row_arg, w.label0, w.keep, w.sampled, label, reg);
     FRCNN_LAUNCH_CHECK("at_finish_kernel");
     if (argmax && hipMemcpyAsync(argmax, w.row_arg, sizeof(int32_t) * N * A,
                                  hipMemcpyDeviceToDevice, st) != hipSuccess)
-        return check_launch("frcnn_anchor_target copy");
+        return check_launch("frcnn_anchor_target_sample copy");
     if (max_iou && hipMemcpyAsync(max_iou, w.row_max, sizeof(double) * N * A,
                                   hipMemcpyDeviceToDevice, st) != hipSuccess)
-        return check_launch("frcnn_anchor_target copy");
+        return check_launch("frcnn_anchor_target_sample copy");
     return FRCNN_OK;
+}
+
+extern "C" int frcnn_anchor_target(int N, int A, int G, const float* anchors, const double* boxes,
+                                   const double* labels, int n_sample, double pos_iou_thresh,
+                                   double neg_iou_thresh, double pos_ratio, uint32_t* rng_state,
+                                   double* reg, int32_t* label, int32_t* argmax, double* max_iou,
+                                   void* workspace, size_t ws_bytes, void* stream) {
+    FRCNN_REQUIRE(anchors && reg && label, "frcnn_anchor_target: null pointer");
+    const int n_pos_max = static_cast<int>(pos_ratio * n_sample);
+    FRCNN_REQUIRE(n_sample - (n_pos_max < 0 ? 0 : n_pos_max) <= kMaxKeep && n_pos_max <= kMaxKeep,
+                  "frcnn_anchor_target: n_sample too large");
+    int rc = frcnn_anchor_target_prepare(N, A, G, anchors, boxes, labels, pos_iou_thresh, neg_iou_thresh,
+                                         workspace, ws_bytes, stream);
+    if (rc != FRCNN_OK) return rc;
+    return frcnn_anchor_target_sample(N, A, G, anchors, n_sample, pos_ratio, rng_state, reg, label, argmax,
+                                      max_iou, workspace, ws_bytes, stream);
 }
 
 namespace {

@@ -61,6 +61,66 @@ def anchor_targets(boxes, labels, anchors, n_sample=256, pos_iou_thresh=0.7, neg
     return reg, lab
 
 
+class AnchorTargetPlan:
+    """The RNG-free half of AnchorTargetCreator (anchor_targets_prepare): the
+    gt, IoU, labels and candidate lists in a workspace, ready for the draws."""
+
+    def __init__(self, N, A, G, anchors, boxes, labels, ws):
+        self.N, self.A, self.G = N, A, G
+        self.anchors, self.boxes, self.labels, self.ws = anchors, boxes, labels, ws
+
+
+def anchor_targets_workspace(N, A, G, device=None):
+    """A workspace for anchor_targets_prepare / _sample (caller-owned, so a
+    training loop can double-buffer plans across streams)."""
+    lib = _lib.load()
+    return torch.empty(max(int(lib.frcnn_anchor_target_workspace_size(N, A, G)), 1), dtype=torch.uint8,
+                       device=device if device is not None else _lib.device())
+
+
+def anchor_targets_prepare(boxes, labels, anchors, pos_iou_thresh=0.7, neg_iou_thresh=0.3, workspace=None):
+    """First half of ``anchor_targets`` (utils/utils.py:146-188: IoU, labels,
+    candidate lists) on the current stream; uses no RNG, so it can run ahead of
+    the previous step's draws on another stream."""
+    lib = _lib.load()
+    dev = _lib.device()
+    b, l = _gt(boxes, labels, dev)
+    a = (anchors if isinstance(anchors, torch.Tensor) else torch.as_tensor(np.asarray(anchors, np.float32)))
+    a = a.to(dev, torch.float32).contiguous()
+    N, G = b.shape[:2]
+    A = a.size(0)
+    ws = workspace if workspace is not None else anchor_targets_workspace(N, A, G, dev)
+    _lib.check(lib.frcnn_anchor_target_prepare(N, A, G, _lib.ptr(a), _lib.ptr(b), _lib.ptr(l),
+                                               float(pos_iou_thresh), float(neg_iou_thresh), _lib.ptr(ws),
+                                               ws.numel(), _lib.stream_ptr()), "anchor_target_prepare")
+    return AnchorTargetPlan(N, A, G, a, b, l, ws)
+
+
+def anchor_targets_sample(plan, n_sample=256, pos_ratio=0.5, rng=None, out=None):
+    """Second half of ``anchor_targets``: the np.random.choice draws (numpy's
+    global RNG, or the device stream ``rng``) and the regression targets, on the
+    current stream, after ``plan``'s prepare (order the streams with an event).
+    ``out`` = caller-owned (reg fp64 [N,A,4], label int32 [N,A])."""
+    lib = _lib.load()
+    dev = plan.ws.device
+    N, A, G = plan.N, plan.A, plan.G
+    if out is None:
+        reg = torch.empty((N, A, 4), dtype=torch.float64, device=dev)
+        lab = torch.empty((N, A), dtype=torch.int32, device=dev)
+    else:
+        reg, lab = out
+    own = rng is None
+    if own:
+        rng, st = rng_state_to_device(dev)
+    _lib.check(lib.frcnn_anchor_target_sample(N, A, G, _lib.ptr(plan.anchors), int(n_sample), float(pos_ratio),
+                                              _lib.ptr(rng), _lib.ptr(reg), _lib.ptr(lab), None, None,
+                                              _lib.ptr(plan.ws), plan.ws.numel(), _lib.stream_ptr()),
+               "anchor_target_sample")
+    if own:
+        rng_state_from_device(rng, st)
+    return reg, lab
+
+
 def proposal_targets(rois, rcount, boxes, labels, n_sample=128, pos_ratio=0.5, pos_iou_thresh=0.5,
                      neg_iou_thresh_high=0.5, neg_iou_thresh_low=0.0,
                      reg_normalize_mean=(0., 0., 0., 0.), reg_normalize_std=(0.1, 0.1, 0.2, 0.2),

@@ -227,3 +227,32 @@ def test_anchor_targets_from_voc_annotations(rng_guard):
         assert np.array_equal(lab[i].cpu().numpy(), olab)
         np.testing.assert_allclose(reg[i].cpu().numpy(), oreg, rtol=1e-12, atol=0)
     assert np.array_equal(np.random.get_state()[1], st[1]) and np.random.get_state()[2] == st[2]
+
+
+def test_anchor_targets_prepare_sample_split(rng_guard):
+    """anchor_targets_prepare (on a side stream) + anchor_targets_sample == the
+    one-call anchor_targets: same labels, regression targets and RNG stream."""
+    N, G, img = 3, 32, 600
+    anchors = torch.from_numpy(orc.generate_anchors(orc.generate_anchor_base(), 16, 38, 38)).cuda()
+    bl = [synth.gt_boxes(img, img, G, 8, i, n_valid=[32, 4, 0][i]) for i in range(N)]
+    boxes = torch.from_numpy(np.stack([b for b, _ in bl])).cuda()
+    labels = torch.from_numpy(np.stack([l for _, l in bl])).cuda()
+    np.random.seed(17)
+    rng_a, _ = U.rng_state_to_device(torch.device("cuda"))
+    ref = [targets.anchor_targets(boxes, labels, anchors, rng=rng_a) for _ in range(2)]
+    np.random.seed(17)
+    rng_b, _ = U.rng_state_to_device(torch.device("cuda"))
+    side = torch.cuda.Stream()
+    got = []
+    for _ in range(2):
+        with torch.cuda.stream(side):
+            plan = targets.anchor_targets_prepare(boxes, labels, anchors)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        torch.cuda.current_stream().wait_event(ev)
+        got.append(targets.anchor_targets_sample(plan, rng=rng_b))
+    torch.cuda.synchronize()
+    for (r0, l0), (r1, l1) in zip(ref, got):
+        assert torch.equal(l0, l1)
+        assert torch.equal(r0, r1)
+    assert torch.equal(rng_a, rng_b)
