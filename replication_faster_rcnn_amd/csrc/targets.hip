@@ -288,7 +288,9 @@ __device__ unsigned long long g_samp_prof[16];
 #define SPROF_ADD(k, v) do {} while (0)
 #define SPROF_DT(k) do {} while (0)
 #endif
-constexpr int kRing = 3;  // a window (<= 1024 words from pos <= 624) spans <= 3 blocks
+constexpr int kWinWaves = 12;              // waves that walk a window; the other 4 twist ahead
+constexpr int kWin = kWinWaves * 64;       // words per window
+constexpr int kRing = 4;  // a window (768 words from pos <= 624) spans <= 3 blocks, + 1 being twisted
 #ifndef FRCNN_SEQ_BELOW
 #define FRCNN_SEQ_BELOW 1024
 #endif
@@ -313,9 +315,8 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
 
 // numpy's mt19937_gen: nw = the state block after old (words i < 227 read
 // old[i + 397], later words the new word 227 before them; word 623 reads the
-// new word 0).
-__device__ __forceinline__ void mt_twist(const uint32_t* __restrict__ old, uint32_t* __restrict__ nw) {
-    const int t = threadIdx.x;
+// new word 0).  Threads t = 0..226 of the caller's group do the work.
+__device__ __forceinline__ void mt_twist(const uint32_t* __restrict__ old, uint32_t* __restrict__ nw, int t) {
     if (t < kMtN - kMtM) {
         const uint32_t a = old[t + kMtM] ^ mt_mix(old[t], old[t + 1]);
         const uint32_t b = a ^ mt_mix(old[t + 227], old[t + 228]);
@@ -358,17 +359,22 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     int i_cur = i_hi;
     while (i_cur >= 1) {
-        const int need = (st.off + kSampThreads - 1) / kMtN;  // blocks past st.slot this window reaches
+        const int need = (st.off + kWin - 1) / kMtN;  // blocks past st.slot this window reaches
         {
             SPROF_T0();
-            while (st.ngen < need) {
-                mt_twist(S.ring[(st.slot + st.ngen) % kRing], S.ring[(st.slot + st.ngen + 1) % kRing]);
+            while (st.ngen < need) {  // (only when the twisting waves fell behind)
+                mt_twist(S.ring[(st.slot + st.ngen) % kRing], S.ring[(st.slot + st.ngen + 1) % kRing], tid);
                 __syncthreads();
                 ++st.ngen;
                 SPROF_ADD(1, 1);
             }
             SPROF_DT(2);
         }
+        // waves kWinWaves.. twist the next block into a free ring slot while the
+        // others walk the window; the window's barriers publish it
+        const bool gen = st.ngen < kRing - 1;
+        if (gen && wid >= kWinWaves)
+            mt_twist(S.ring[(st.slot + st.ngen) % kRing], S.ring[(st.slot + st.ngen + 1) % kRing], tid - kWin);
         SPROF_ADD(0, 1);
         SPROF_T0();
         if (i_cur < kSeqBelow) {
@@ -377,7 +383,7 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
             // chunks in order, each solved exactly on the known step.
             if (wid == 0) {
                 int i_loc = i_cur, used = 0;
-                for (int c = 0; c < kSampWaves && i_loc >= 1; ++c) {
+                for (int c = 0; c < kWinWaves && i_loc >= 1; ++c) {
                     const int gc = st.off + 64 * c + lane;
                     const int bc = gc / kMtN;
                     const uint32_t wc = mt_temper(S.ring[(st.slot + bc) % kRing][gc - bc * kMtN]);
@@ -415,6 +421,7 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
             SPROF_DT(10);
             const int i_new = S.last[0], consumed = S.last[1];
             i_cur = i_new;
+            if (gen) ++st.ngen;
             st.off += consumed;
             while (st.off > kMtN) {
                 st.off -= kMtN;
@@ -424,7 +431,7 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
             __syncthreads();
             continue;
         }
-        const int g = st.off + tid;
+        const int g = st.off + (wid < kWinWaves ? tid : 0);
         const int blk = g / kMtN;
         const uint32_t w = mt_temper(S.ring[(st.slot + blk) % kRing][g - blk * kMtN]);
         const float p_acc = (static_cast<float>(i_cur) + 1.0f) /
@@ -446,7 +453,7 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
         // settle there; each round settles at least one more wave.
         int il = 0, total = 0, par = 0;
         uint32_t m = 0;
-        bool a = false, done = false;
+        bool a = false, done = wid >= kWinWaves;  // the twisting waves only keep the barriers
         for (int round = 0;; ++round) {
             if (!done) {
                 for (;;) {  // this wave's 64 words, exact for the assumed `base`
@@ -479,16 +486,16 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
                 dn = __ockl_wfred_min_u32(dn);
                 up = __ockl_wfred_min_u32(up);
             }
-            if (lane == 0)
+            if (lane == 0 && wid < kWinWaves)
                 S.rec[par][wid] = make_int4(__popcll(acc), static_cast<int>(dn), static_cast<int>(up), base);
             __syncthreads();
-            const int4 r = lane < kSampWaves ? S.rec[par][lane] : make_int4(0, 0, 0, 0);
+            const int4 r = lane < kWinWaves ? S.rec[par][lane] : make_int4(0, 0, 0, 0);
             const int incl = row16_scan_add(r.x);  // lanes 0..15: prefix over waves
             const int excl = incl - r.x;
             const int d = excl - r.w;  // exact base - assumed base of wave `lane`
-            const uint64_t bad = __ballot(lane < kSampWaves && (d > r.y || -d > r.z));
-            const int first_bad = bad ? __ffsll(static_cast<unsigned long long>(bad)) - 1 : kSampWaves;
-            const int my_excl = __builtin_amdgcn_readlane(excl, wid);
+            const uint64_t bad = __ballot(lane < kWinWaves && (d > r.y || -d > r.z));
+            const int first_bad = bad ? __ffsll(static_cast<unsigned long long>(bad)) - 1 : kWinWaves;
+            const int my_excl = __builtin_amdgcn_readlane(excl, wid < kWinWaves ? wid : 0);
             if (wid < first_bad) {
                 if (!done) {  // settled: same pattern at the exact base, steps shifted
                     il -= my_excl - base;
@@ -498,20 +505,21 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
             } else {
                 base = my_excl;
             }
-            total = __builtin_amdgcn_readlane(incl, kSampWaves - 1);
+            total = __builtin_amdgcn_readlane(incl, kWinWaves - 1);
             par ^= 1;
             SPROF_ADD(3, 1);
-            if (first_bad == kSampWaves) break;
+            if (first_bad == kWinWaves) break;
         }
         SPROF_DT(4);
         if (a && il >= rec_lo) J[il - rec_lo] = static_cast<int>(w & m);
-        int consumed = kSampThreads;
+        int consumed = kWin;
         if (i_cur - total < 1) {  // the call ends inside this window
-            if (lane == 0) S.last[wid] = acc ? 64 * wid + 64 - __clzll(acc) : 0;
+            if (lane == 0 && wid < kWinWaves) S.last[wid] = acc ? 64 * wid + 64 - __clzll(acc) : 0;
             __syncthreads();
-            consumed = static_cast<int>(__ockl_wfred_max_u32(lane < kSampWaves ? static_cast<uint32_t>(S.last[lane]) : 0u));
+            consumed = static_cast<int>(__ockl_wfred_max_u32(lane < kWinWaves ? static_cast<uint32_t>(S.last[lane]) : 0u));
         }
         i_cur -= total;
+        if (gen) ++st.ngen;
         st.off += consumed;
         while (st.off > kMtN) {  // pos == 624 stays in its block, like numpy
             st.off -= kMtN;
