@@ -535,9 +535,8 @@ __device__ unsigned int g_pool_prof_rois[kPoolProfSlots];
         if (_wg < kPoolProfSlots) {                                                                 \
             if ((k) == 3) {                                                                         \
                 if ((threadIdx.x & 63) == 0) atomicMax(&g_pool_prof[_wg][3], _t);                   \
-            } else if (threadIdx.x == 0) {                                                          \
-                g_pool_prof[_wg][k] = _t;                                                           \
             }                                                                                       \
+            else if (threadIdx.x == 0) g_pool_prof[_wg][k] = _t;                                    \
         }                                                                                           \
     } while (0)
 #define PPROF_ROIS(n)                                                                               \
@@ -550,29 +549,59 @@ __device__ unsigned int g_pool_prof_rois[kPoolProfSlots];
 #define PPROF_ROIS(n) do {} while (0)
 #endif
 
-// Tile layout of the wave-per-RoI forward: 16-pixel groups, the group's NP
-// 4-channel planes back to back (pixel p of plane q at float4
-// (g*NP + q)*16 + s, g = p >> 4), the slot s = (p ^ g) & 15 XOR-swizzled so
-// that a ds_read_b128 of bins a bin width apart does not collide, and the
-// planes of one pixel 256 B apart -- LDS immediate offsets.
-template <int NP>
-__device__ __forceinline__ const float4* tile_px(const float4* q4, int p) {
-    const int g = p >> 4;
-    return q4 + g * (NP * 16) + ((p ^ g) & 15);
+// Lane -> bin of the wave-per-RoI forward.  A ds_read_b128 is serviced in four
+// 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32), and
+// only lanes of one group conflict.  With PH, PW <= 8 group k takes the bins
+// of bin rows 2k and 2k+1: two window rows a bin height apart, the columns of
+// one row a bin width apart -- fewer colliding 16-B slots than bin = lane
+// (simulated on cfg2's RoIs: 1.61 vs 1.76 LDS cycles per group).  -1 = idle.
+__device__ __forceinline__ int wave_lane_bin(int lane, int PH, int PW) {
+    if (PH > 8 || PW > 8) return lane < PH * PW ? lane : -1;
+    const int r = lane & 31;
+    int grp, pos;
+    if (r < 4) { grp = 0; pos = r; }
+    else if (r < 12) { grp = 1; pos = r - 4; }
+    else if (r < 16) { grp = 0; pos = r - 8; }
+    else if (r < 20) { grp = 1; pos = r - 8; }
+    else if (r < 28) { grp = 0; pos = r - 12; }
+    else { grp = 1; pos = r - 16; }
+    const int k = (lane >> 5) * 2 + grp;
+    if (pos >= 2 * PW) return -1;
+    const int ph = 2 * k + pos / PW;
+    return ph < PH ? ph * PW + pos % PW : -1;
+}
+
+// Pixels per plane of the wave kernel's tile: HW + the sentinel, 16-aligned.
+__host__ __device__ constexpr int wave_tile_pixels(int HW) { return (HW + 16) & ~15; }  // + sentinel
+
+__device__ __forceinline__ void lds_barrier() {
+    // LDS handoff only: a bare s_barrier after the wave's LDS ops complete, so
+    // global loads issued before it stay in flight (no vmcnt drain)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // ------------------------------------------------- wave-per-RoI forward
 // The default forward for RoIs grouped by image.  Grid (C/CG, split, N + 1):
 // one 1024-thread workgroup owns CG channel planes of one image (staged once
-// into LDS, tile_px layout) and a strided
-// share of that image's RoIs (items z, z+split, ...: RoI sizes are
-// uncorrelated with rank, so every share sees the image's size mix).  One
-// wave per RoI, lane = bin: each lane walks its window once and updates CG
-// (max, first index) pairs with torchvision's strict '>' -- the RoI geometry,
-// the window walk and the pixel address are shared by CG channels.  Waves pull
-// RoIs from an LDS counter (RoI sizes vary 100x); the RoI geometry of a chunk
-// of RoIs is computed once per workgroup into LDS.  Output: per channel, the
-// 49 lanes write one contiguous 196-B run.
+// into LDS) and a strided share of that image's RoIs (items z, z+split, ...:
+// RoI sizes are uncorrelated with rank, so every share sees the image's size
+// mix).  One wave per RoI, lane = bin (wave_lane_bin): the RoI geometry, the
+// window walk and the pixel address are shared by CG channels.
+//  * tile: NP = CG/4 float4 planes, plane q = channels 4q..4q+3, pixel p at
+//    q4[q*HWs + p] -- a pixel's address is linear in p, so a pixel pair costs
+//    a few address VALU; NaN staged as -inf (never selected by the strict '>'
+//    against the -FLT_MAX start, and max3 never sees a NaN);
+//  * scan: each lane walks its window row by row in pixel pairs (a, b = next
+//    pixel, clamped to the row end); per channel m' = max3(m, a, b) and the
+//    pair is recorded iff m' > m (3 VALU per pair instead of 3 per pixel).
+//    A strict increase can only happen at the pair holding the row-major
+//    first maximum, so after the scan the argmax is a if tile[a] == m, else b
+//    = a + 1 -- torchvision's strict-'>' first max, exactly; the value is
+//    re-read from the tile, so a zero maximum keeps its sign;
+//  * prologue: the tile's global loads, the image's RoI range and the first
+//    geometry chunk's box loads are all in flight together;
+//  * waves pull RoIs from an LDS counter (RoI sizes vary 100x); per channel the
+//    bins of a RoI are one contiguous 4*PH*PW-B run of out / argmax.
 // HEAD: fused with the head's RoI transform (nets/heads.py:42-47): `rois` are
 // the [R,4] image boxes, hd.inds their image index; the [idx, box] rows are
 // formed in registers and (channel group 0) written to hd.boxes.  The image
@@ -581,19 +610,23 @@ __device__ __forceinline__ const float4* tile_px(const float4* q4, int p) {
 // after every real one instead of holding CUs between them.
 // (Measured alternatives -- RoI bins packed 64 per wave, bins sorted by window
 // shape per image or per RoI block -- are slower: DESIGN.md §3.)
-template <int NT, int CG, bool HEAD>
+constexpr int kStageUnroll = 3;  // pixel rounds of tile loads in flight per thread
+
+template <int NT, int CG, int FIX, bool HEAD>
 __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
-    const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W, int PH, int PW,
+    const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W, int PH_, int PW_,
     float ss, float* __restrict__ out, int32_t* __restrict__ argmax, int geo_cap, HeadArgs hd) {
     constexpr int NP = CG / 4;
     extern __shared__ __attribute__((aligned(16))) float4 q4[];  // plane k at q4 + k * HWs; geometry after
     __shared__ int s_red[2 * (NT / 64)];
     __shared__ int s_next;
+    const int PH = FIX ? FIX : PH_, PW = FIX ? FIX : PW_;
     const int b = blockIdx.z;
     const int c0 = blockIdx.x * CG;
     const int tid = threadIdx.x, lane = tid & 63;
     const int HW = H * W;
-    const int HWs = (HW + 15) & ~15;
+    const int HWs = wave_tile_pixels(HW);
+    const int S = HW;  // sentinel pixel: NaN in every plane (max3 ignores it)
     const int PHW = PH * PW;
     const int split = gridDim.y, z = blockIdx.y;
     const int N = gridDim.z - 1;
@@ -622,46 +655,124 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
         }
         return;
     }
-    const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, b, b + 1, s_red, 1)
-                         : roi_range_sorted<NT>(rois, R, b, b + 1, s_red);
-    const int rbase = rg.x, nr = rg.y - rg.x;
+    // ---- prologue: the RoI-range loads, then the first rounds of tile loads
+    // (unconditional: clamped addresses), then the range reduction (waits for
+    // its own loads only), then the first geometry chunk's box loads; the tile
+    // writes wait for the tile loads.
+    int c_lo = 0, c_hi = 0;
+    {
+        const float* bi = HEAD ? hd.inds : rois;
+        const int stride = HEAD ? 1 : 5;
+        for (int r = tid; r < R; r += NT) {
+            const int rb = static_cast<int>(bi[static_cast<size_t>(r) * stride]);
+            c_lo += rb < b;
+            c_hi += rb < b + 1;
+        }
+    }
+    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+    float v[kStageUnroll][CG];
+    auto stage_load = [&](int p0) {
+#pragma unroll
+        for (int u = 0; u < kStageUnroll; ++u) {
+            const int p = min(p0 + u * NT, HW - 1);
+#pragma unroll
+            for (int q = 0; q < CG; ++q) v[u][q] = src[static_cast<size_t>(q) * HW + p];
+        }
+    };
+    auto stage_store = [&](int p0) {
+#pragma unroll
+        for (int u = 0; u < kStageUnroll; ++u) {
+            const int p = p0 + u * NT;
+            if (p < HW) {
+#pragma unroll
+                for (int k = 0; k < NP; ++k) {
+                    float e[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float t = v[u][4 * k + j];
+                        e[j] = t != t ? -INFINITY : t;
+                    }
+                    q4[k * HWs + p] = make_float4(e[0], e[1], e[2], e[3]);
+                }
+            }
+        }
+    };
+    stage_load(tid);
+    for (int o = 32; o > 0; o >>= 1) {
+        c_lo += __shfl_xor(c_lo, o, 64);
+        c_hi += __shfl_xor(c_hi, o, 64);
+    }
+    if (lane == 0) {
+        s_red[2 * (tid >> 6)] = c_lo;
+        s_red[2 * (tid >> 6) + 1] = c_hi;
+    }
+    if (tid < NP) q4[tid * HWs + S] = make_float4(NAN, NAN, NAN, NAN);
+    lds_barrier();
+    c_lo = c_hi = 0;
+    for (int w = 0; w < NT / 64; ++w) {
+        c_lo += s_red[2 * w];
+        c_hi += s_red[2 * w + 1];
+    }
+    const int rbase = c_lo, nr = c_hi - c_lo;
     PPROF_T(1);
-    if (z >= nr) return;
+    if (z >= nr) return;  // uniform; no barrier below is skipped by part of the group
     const int nmine = (nr - z + split - 1) / split;  // items z, z+split, ...
     PPROF_ROIS(nmine);
-    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
-    for (int p = tid; p < HW; p += NT) {
-        float v[CG];
-#pragma unroll
-        for (int q = 0; q < CG; ++q) {
-            const float e = src[static_cast<size_t>(q) * HW + p];
-            v[q] = e;
-        }
-        const float4* pp = tile_px<NP>(q4, p);
-#pragma unroll
-        for (int k = 0; k < NP; ++k)
-            const_cast<float4*>(pp)[16 * k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
-    }
     int4* s_geo = reinterpret_cast<int4*>(q4 + NP * HWs);
-    const int ph = lane / PW, pw = lane - (lane / PW) * PW;
-    const bool act = lane < PHW;
+    int* s_dim = reinterpret_cast<int*>(s_geo + geo_cap);
+    // the first geometry chunk's boxes, loaded before the tile is written
+    float bx0[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    if (tid < min(geo_cap, nmine)) {
+        const int r = rbase + z + tid * split;
+        if (HEAD) {
+            head_box(rois, hd, r, bx0);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 5; ++j) bx0[j] = rois[static_cast<size_t>(r) * 5 + j];
+        }
+    }
+    stage_store(tid);
+    for (int p0 = tid + kStageUnroll * NT; p0 < HW; p0 += kStageUnroll * NT) {
+        stage_load(p0);
+        stage_store(p0);
+    }
+
+    const int bin = wave_lane_bin(lane, PH, PW);
+    const bool act = bin >= 0;
+    const int ph = act ? bin / PW : 0, pw = act ? bin - (bin / PW) * PW : 0;
+    const uint32_t plane_bytes = static_cast<uint32_t>(HWs) * 16u;
+    const char* tb = reinterpret_cast<const char*>(q4);
     for (int k0 = 0; k0 < nmine; k0 += geo_cap) {
         const int cn = min(geo_cap, nmine - k0);
         for (int i = tid; i < cn; i += NT) {
-            const int r = rbase + z + (k0 + i) * split;
             float bx[5];
-            if (HEAD) {
-                head_box(rois, hd, r, bx);
-                if (hd.boxes && blockIdx.x == 0) {
+            const int r = rbase + z + (k0 + i) * split;
+            if (k0 == 0 && i == tid) {
 #pragma unroll
-                    for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
-                }
+                for (int j = 0; j < 5; ++j) bx[j] = bx0[j];
+            } else if (HEAD) {
+                head_box(rois, hd, r, bx);
             } else {
 #pragma unroll
                 for (int j = 0; j < 5; ++j) bx[j] = rois[static_cast<size_t>(r) * 5 + j];
             }
+            if (HEAD && hd.boxes && blockIdx.x == 0) {
+#pragma unroll
+                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
+            }
             const RoiGeom gm = roi_geom(bx, ss, PH, PW);
             s_geo[i] = make_int4(gm.sh, gm.sw, __float_as_int(gm.bh), __float_as_int(gm.bw));
+            // the RoI's tallest / widest bin window: the wave's uniform walk
+            int hm = 0, wm = 0;
+            for (int t = 0; t < PH; ++t) {
+                const int4 g = geom_bin(gm, H, W, t, 0);
+                hm = max(hm, g.y - g.x);
+            }
+            for (int t = 0; t < PW; ++t) {
+                const int4 g = geom_bin(gm, H, W, 0, t);
+                wm = max(wm, g.w - g.z);
+            }
+            s_dim[i] = (wm > 0 ? hm : 0) | (hm > 0 ? wm : 0) << 16;  // Hm | Wm << 16
         }
         if (tid == 0) s_next = 0;
         __syncthreads();
@@ -674,51 +785,126 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
             if (lane == 0) kn = atomicAdd(&s_next, 1);  // prefetch the next item
             const int r = rbase + z + (k0 + k) * split;
             const int4 gq = s_geo[k];
+            const int dim = __builtin_amdgcn_readfirstlane(s_dim[k]);
+            const int Hm = dim & 0xffff, Wm = dim >> 16;
             RoiGeom gm;
             gm.sh = gq.x;
             gm.sw = gq.y;
             gm.bh = __int_as_float(gq.z);
             gm.bw = __int_as_float(gq.w);
-            int4 g = geom_bin(gm, H, W, ph, pw);
-            if (!act) g = make_int4(0, 0, 0, 0);
-            const bool empty = g.y <= g.x || g.w <= g.z;
-            float mv[CG];
-            int mi[CG];
+            const int4 g = geom_bin(gm, H, W, ph, pw);
+            const bool empty = !act || g.y <= g.x || g.w <= g.z;
+            // the lane's window: rows past its last are masked off (a row ends
+            // with the maxima in mv), a pair's b past its last column is its a
+            // (a repeated pixel never passes the strict '>' again); an empty
+            // window is one row of one column: the sentinel pixel, which max3
+            // ignores
+            const int hh = empty ? 1 : g.y - g.x;
+            const int ww = empty ? 1 : g.w - g.z;
+            const int p00 = empty ? S : g.x * W + g.z;
+            const int rstep = empty ? 0 : W;
+            const float init = empty ? 0.0f : -FLT_MAX;
+            float mv[CG], m2[CG];
+            int mi[CG];  // pixel a of the pair of the last strict increase (-2: none)
+            // one pixel pair at row pixel rowp, columns k and k+1 (uniform k):
+            // per channel m' = max3(m, a, b), record a iff m' > m; FIRST: m =
+            // init for every channel (no per-channel initialisation)
+            auto pair = [&](const float (&s)[CG], float (&d)[CG], int rowp, int k, bool first) {
+                const int pa = rowp + k;
+                const int pb = k + 1 < ww ? pa + 1 : pa;
+                const char* aa = tb + (static_cast<uint32_t>(pa) << 4);
+                const char* ab = tb + (static_cast<uint32_t>(pb) << 4);
+                float4 va[NP], vb[NP];
 #pragma unroll
-            for (int c = 0; c < CG; ++c) {
-                mv[c] = empty ? 0.0f : -FLT_MAX;
-                mi[c] = -1;
-            }
-            for (int h = g.x; h < g.y; ++h) {
-                const int rb = h * W;
-                for (int w = g.z; w < g.w; ++w) {
-                    const int ii = rb + w;
-                    const float4* pp = tile_px<NP>(q4, ii);
-                    float4 v[NP];
+                for (int q = 0; q < NP; ++q) {
+                    va[q] = *static_cast<const float4*>(__builtin_assume_aligned(aa + q * plane_bytes, 16));
+                    vb[q] = *static_cast<const float4*>(__builtin_assume_aligned(ab + q * plane_bytes, 16));
+                }
 #pragma unroll
-                    for (int q = 0; q < NP; ++q) v[q] = pp[16 * q];
-                    // all NP reads in flight before the first compare (else the compiler
-                    // waits on each read in turn: NP LDS round trips per pixel)
-                    __builtin_amdgcn_sched_barrier(0);
+                for (int q = 0; q < NP; ++q) {
+                    const float a4[4] = {va[q].x, va[q].y, va[q].z, va[q].w};
+                    const float b4[4] = {vb[q].x, vb[q].y, vb[q].z, vb[q].w};
 #pragma unroll
-                    for (int q = 0; q < NP; ++q) {
-                        const float vv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+                    for (int j = 0; j < 4; ++j) {
+                        const int c = 4 * q + j;
+                        const float m0 = first ? init : s[c];
+                        const float m = max3_raw(m0, a4[j], b4[j]);
+                        mi[c] = m > m0 ? pa : (first ? -2 : mi[c]);
+                        d[c] = m;
+                    }
+                }
+            };
+            if (Hm > 0) {
+                // row 0 (every lane): the first pair initialises mv / mi
+                pair(mv, mv, p00, 0, true);
+                int kk = 2;
+                for (; kk + 2 < Wm; kk += 4) {  // two pairs per trip: mv -> m2 -> mv
+                    pair(mv, m2, p00, kk, false);
+                    pair(m2, mv, p00, kk + 2, false);
+                }
+                if (kk < Wm) {  // odd last pair of the row (uniform)
+                    pair(mv, m2, p00, kk, false);
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            if (vv[j] > mv[4 * q + j]) {  // torchvision's strict '>'
-                                mv[4 * q + j] = vv[j];
-                                mi[4 * q + j] = ii;
-                            }
+                    for (int c = 0; c < CG; ++c) mv[c] = m2[c];
+                }
+                for (int i = 1; i < Hm; ++i) {
+                    if (i < hh) {  // ragged last rows: lanes past their last row are masked
+                        const int rowp = p00 + i * rstep;
+                        int k2 = 0;
+                        for (; k2 + 2 < Wm; k2 += 4) {
+                            pair(mv, m2, rowp, k2, false);
+                            pair(m2, mv, rowp, k2 + 2, false);
+                        }
+                        if (k2 < Wm) {
+                            pair(mv, m2, rowp, k2, false);
+#pragma unroll
+                            for (int c = 0; c < CG; ++c) mv[c] = m2[c];
                         }
                     }
                 }
-            }
-            if (act) {
-                const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
+            } else {  // every bin empty (RoI outside the map)
 #pragma unroll
                 for (int c = 0; c < CG; ++c) {
-                    out[o + static_cast<size_t>(c) * PHW] = mv[c];
-                    argmax[o + static_cast<size_t>(c) * PHW] = mi[c];
+                    mv[c] = init;
+                    mi[c] = -2;
+                }
+            }
+            // argmax = a if tile[a] == m (a comes first), else b = a + 1; the
+            // value is tile[a]'s bits, or m's; m's bits can differ from b's only
+            // for a zero maximum (max3 may return either zero): re-read b then
+            float va[CG];
+#pragma unroll
+            for (int c = 0; c < CG; ++c) {
+                const uint32_t pa = min(static_cast<uint32_t>(mi[c]), static_cast<uint32_t>(S));
+                va[c] = reinterpret_cast<const float*>(tb + (c >> 2) * plane_bytes + (pa << 4))[c & 3];
+            }
+            bool zfix = false;
+            int idx[CG];
+#pragma unroll
+            for (int c = 0; c < CG; ++c) {
+                const bool ne = va[c] != mv[c];
+                zfix |= ne && mv[c] == 0.0f && mi[c] >= 0;
+                va[c] = ne ? mv[c] : va[c];
+                idx[c] = mi[c] + (ne ? 1 : 0);
+            }
+            if (__builtin_amdgcn_ballot_w64(zfix)) {  // rare: a zero maximum first met at b
+#pragma unroll
+                for (int c = 0; c < CG; ++c)
+                    if (mv[c] == 0.0f && mi[c] >= 0 && idx[c] != mi[c])
+                        va[c] = reinterpret_cast<const float*>(tb + (c >> 2) * plane_bytes +
+                                                               (static_cast<uint32_t>(idx[c]) << 4))[c & 3];
+            }
+#ifdef FRCNN_POOL_NOSTORE
+            if (act && r < 0) {  // probe build: the scan without its output stores
+#else
+            if (act) {
+#endif
+                float* op = out + (static_cast<size_t>(r) * C + c0) * PHW + bin;
+                int32_t* ap = argmax + (static_cast<size_t>(r) * C + c0) * PHW + bin;
+#pragma unroll
+                for (int c = 0; c < CG; ++c) {
+                    op[c * PHW] = va[c];
+                    ap[c * PHW] = idx[c];
                 }
             }
             k = __builtin_amdgcn_readfirstlane(kn);
@@ -1131,8 +1317,9 @@ PxPlan px_plan(int C, int N, int H, int W, int PHW, hipStream_t st) {
     const size_t HW = static_cast<size_t>(H) * W;
     if (N <= 0 || HW == 0 || PHW > 64 || H > 65535 || W > 65535) return pl;
     constexpr size_t kReserve = 1024;  // static LDS + allocation rounding
-    constexpr size_t kMinGeo = 64 * sizeof(int4);
-    const size_t HWs = (HW + 15) & ~static_cast<size_t>(15);
+    constexpr size_t kGeoItem = sizeof(int4) + sizeof(int);  // s_geo + s_dim
+    constexpr size_t kMinGeo = 64 * kGeoItem;
+    const size_t HWs = static_cast<size_t>(wave_tile_pixels(static_cast<int>(HW)));
     for (int cg : {16, 8, 4}) {
         if (C % cg != 0) continue;
         if (path_cfg().roi_cg && cg != path_cfg().roi_cg) continue;  // A/B override
@@ -1141,10 +1328,10 @@ PxPlan px_plan(int C, int N, int H, int W, int PHW, hipStream_t st) {
         if (2 * (tile + kMinGeo + kReserve) <= kLdsPerCu) per_cu = 2;
         else if (tile + kMinGeo + kReserve <= kLdsPerCu) per_cu = 1;
         if (!per_cu) continue;
-        const size_t geo = (kLdsPerCu / per_cu - kReserve - tile) / sizeof(int4);
+        const size_t geo = (kLdsPerCu / per_cu - kReserve - tile) / kGeoItem;
         pl.geo_cap = static_cast<int>(geo > 512 ? 512 : geo);
         pl.cg = cg;
-        pl.lds = tile + static_cast<size_t>(pl.geo_cap) * sizeof(int4);
+        pl.lds = tile + static_cast<size_t>(pl.geo_cap) * kGeoItem;
         const int64_t wgs = static_cast<int64_t>(C / cg) * N;
         int64_t sp = (static_cast<int64_t>(stream_cu_count(st)) * per_cu + wgs - 1) / wgs;
         if (path_cfg().roi_split > 0) sp = path_cfg().roi_split;  // A/B override
@@ -1158,12 +1345,17 @@ template <bool HEAD>
 int px_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
               int PH, int PW, float ss, float* out, int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
     const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(pl.split), static_cast<unsigned>(N + 1));
-#define FRCNN_PX(CG)                                                                                    \
-    hipLaunchKernelGGL((roi_pool_fwd_wave_kernel<1024, CG, HEAD>), grid, dim3(1024), pl.lds, st, x, rois, \
+    const bool fix7 = PH == 7 && PW == 7;
+#define FRCNN_PX(CG, FX)                                                                                    \
+    hipLaunchKernelGGL((roi_pool_fwd_wave_kernel<1024, CG, FX, HEAD>), grid, dim3(1024), pl.lds, st, x, rois, \
                        static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd)
-    if (pl.cg == 16) FRCNN_PX(16);
-    else if (pl.cg == 8) FRCNN_PX(8);
-    else FRCNN_PX(4);
+    if (pl.cg == 16) {
+        if (fix7) FRCNN_PX(16, 7); else FRCNN_PX(16, 0);
+    } else if (pl.cg == 8) {
+        if (fix7) FRCNN_PX(8, 7); else FRCNN_PX(8, 0);
+    } else {
+        if (fix7) FRCNN_PX(4, 7); else FRCNN_PX(4, 0);
+    }
 #undef FRCNN_PX
     FRCNN_LAUNCH_CHECK("roi_pool_fwd_wave_kernel");
     return FRCNN_OK;

@@ -34,3 +34,6 @@ print("  ", sys.argv[2], round(d["value"]), "img/s", round(d["ms_per_step"]*1e3,
 PY
   done
 done
+if [ -n "${PROBE:-}" ]; then
+  CFGS="$PROBE" bash tools/gpu_pp.sh "${1:-ablib}/pp" || exit $?
+fi
