@@ -81,6 +81,9 @@ def parse():
                          "gloo (host copies) when ranks share one")
     ap.add_argument("--roi-cg", default="auto",
                     help="channels per RoIPool forward workgroup (frcnn_set_path roi_pool_cg): auto | 4 | 8 | 16")
+    ap.add_argument("--roi-split", default="auto",
+                    help="RoI shares per (image, channel group) of the RoIPool forward "
+                         "(frcnn_set_path roi_pool_split): auto | 1 | 2 | ...")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-baseline sample (rank 0, N=1 only); 0 disables")
     ap.add_argument("--cpu-images", type=int, default=10, help="minimum timed CPU images (median)")
@@ -511,7 +514,8 @@ def main():
     dev = torch.device("cuda", dev_index)
     from replication_faster_rcnn_amd import _lib
     from replication_faster_rcnn_amd import anchors as A
-    for op, v in (("roi_pool_cg", args.roi_cg), ("propose", args.propose_path)):
+    for op, v in (("roi_pool_cg", args.roi_cg), ("roi_pool_split", args.roi_split),
+                  ("propose", args.propose_path)):
         if v != "auto":
             _lib.set_path(op, v)
     from replication_faster_rcnn_amd import dist as fdist
@@ -599,7 +603,7 @@ def main():
         "config": {"workload": workload, "global_batch": n_total,
                    "parallelism": f"dp{world} (per-image sharding)", "streams": args.streams,
                    "prop_streams": args.prop_streams if (args.streams == 2 and not train) else 1,
-                   "host_io": bool(args.host_io), "roi_cg": args.roi_cg,
+                   "host_io": bool(args.host_io), "roi_cg": args.roi_cg, "roi_split": args.roi_split,
                    "prop_cus": args.prop_cus if (args.streams == 2 and not train) else 0,
                    "propose_path": args.propose_path,
                    "collective": (None if world == 1 else

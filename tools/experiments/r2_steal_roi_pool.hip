@@ -1,0 +1,1515 @@
+// RoI max-pooling forward / backward (nets/heads.py:42-48, torchvision
+// roi_pool semantics) on gfx950.
+//
+// Forward, default ("dense"): a workgroup owns CG channel planes of one image,
+// staged once into LDS, and a cost-balanced contiguous share of that image's
+// RoIs.  The share's RoIs are ordered by window size and their PH*PW bins are
+// packed densely into the 64 lanes of each wave (lane = bin of some RoI, so a
+// 7x7 head uses 64/64 lanes instead of 49/64), each lane scanning its bin
+// window for CG channels at once.  The per-channel update takes pixels in
+// pairs: m' = max3(m, a, b), the index moves iff m' > m, to a if a == m' --
+// torchvision's strict-'>' row-major first-max, exactly.
+// Generic: one 256-thread workgroup per RoI (any output size, any layout).
+//
+// Backward: atomic-free, deterministic and bit-identical to the CPU kernel's
+// summation order.  A wave owns one (image, channel) plane in LDS and walks
+// that image's RoIs in ascending order; within one RoI the lanes are the bins;
+// two bins can hit the same pixel only if their windows overlap (mask
+// precomputed per RoI), and such lanes apply their adds in rounds ordered by
+// bin index, so every pixel sees exactly the CPU order n -> ph -> pw.  The
+// finished planes are stored once (zero-fill of grad_in fused).
+#include <cfloat>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+
+#include "common.h"
+
+namespace frcnn {
+
+constexpr int kMaxBins = 1024;
+constexpr size_t kLdsPerCu = 160 * 1024;  // gfx950
+
+// torchvision bin window (hs, he, ws, we) of bin (ph, pw) for RoI `roi`.
+__device__ __forceinline__ int4 roi_bin(const float* roi, float ss, int H, int W, int PH, int PW,
+                                        int ph, int pw) {
+    int sw = static_cast<int>(roundf(roi[1] * ss));
+    int sh = static_cast<int>(roundf(roi[2] * ss));
+    int ew = static_cast<int>(roundf(roi[3] * ss));
+    int eh = static_cast<int>(roundf(roi[4] * ss));
+    int rw = ew - sw + 1;
+    int rh = eh - sh + 1;
+    rw = rw > 1 ? rw : 1;
+    rh = rh > 1 ? rh : 1;
+    float bh = static_cast<float>(rh) / static_cast<float>(PH);
+    float bw = static_cast<float>(rw) / static_cast<float>(PW);
+    int hs = static_cast<int>(floorf(static_cast<float>(ph) * bh)) + sh;
+    int ws = static_cast<int>(floorf(static_cast<float>(pw) * bw)) + sw;
+    int he = static_cast<int>(ceilf(static_cast<float>(ph + 1) * bh)) + sh;
+    int we = static_cast<int>(ceilf(static_cast<float>(pw + 1) * bw)) + sw;
+    hs = min(max(hs, 0), H);
+    he = min(max(he, 0), H);
+    ws = min(max(ws, 0), W);
+    we = min(max(we, 0), W);
+    return make_int4(hs, he, ws, we);
+}
+
+__device__ __forceinline__ void pool_window(const float* __restrict__ plane, int W, int4 g,
+                                            float& mv, int& mi) {
+    mv = (g.y <= g.x || g.w <= g.z) ? 0.0f : -FLT_MAX;
+    mi = -1;
+    for (int h = g.x; h < g.y; ++h) {
+        const float* row = plane + h * W;
+        for (int w = g.z; w < g.w; ++w) {
+            float v = row[w];
+            if (v > mv) {
+                mv = v;
+                mi = h * W + w;
+            }
+        }
+    }
+}
+
+// Generic forward: one workgroup per RoI, window gathers served by L1/L2.
+template <bool VEC>
+__global__ __launch_bounds__(256) void roi_pool_fwd_kernel(const float* __restrict__ x,
+                                                           const float* __restrict__ rois, int N,
+                                                           int C, int H, int W, int PH, int PW,
+                                                           float ss, float* __restrict__ out,
+                                                           int32_t* __restrict__ argmax) {
+    __shared__ int4 bins[kMaxBins];
+    const int r = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int PHW = PH * PW;
+    const float* roi = rois + static_cast<size_t>(r) * 5;
+    for (int k = tid; k < PHW; k += 256) bins[k] = roi_bin(roi, ss, H, W, PH, PW, k / PW, k % PW);
+    __syncthreads();
+    const int b = static_cast<int>(roi[0]);
+    const bool valid = b >= 0 && b < N;
+    const size_t total = static_cast<size_t>(C) * PHW;
+    float* o = out + static_cast<size_t>(r) * total;
+    int32_t* am = argmax + static_cast<size_t>(r) * total;
+    const size_t HW = static_cast<size_t>(H) * W;
+    const float* xb = x + (valid ? static_cast<size_t>(b) * C * HW : 0);
+    if (VEC) {
+        for (size_t e0 = static_cast<size_t>(tid) * 4; e0 < total; e0 += 1024) {
+            int c = static_cast<int>(e0 / PHW);
+            int k = static_cast<int>(e0 - static_cast<size_t>(c) * PHW);
+            float v[4];
+            int m[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (valid) {
+                    pool_window(xb + c * HW, W, bins[k], v[q], m[q]);
+                } else {
+                    v[q] = 0.0f;
+                    m[q] = -1;
+                }
+                if (++k == PHW) {
+                    k = 0;
+                    ++c;
+                }
+            }
+            *reinterpret_cast<float4*>(o + e0) = make_float4(v[0], v[1], v[2], v[3]);
+            *reinterpret_cast<int4*>(am + e0) = make_int4(m[0], m[1], m[2], m[3]);
+        }
+    } else {
+        for (size_t e = tid; e < total; e += 256) {
+            int c = static_cast<int>(e / PHW);
+            int k = static_cast<int>(e - static_cast<size_t>(c) * PHW);
+            float v = 0.0f;
+            int m = -1;
+            if (valid) pool_window(xb + c * HW, W, bins[k], v, m);
+            o[e] = v;
+            am[e] = m;
+        }
+    }
+}
+
+// RoI geometry shared by all bins: start (sh, sw) and bin size (bh, bw).
+struct RoiGeom {
+    int sh, sw;
+    float bh, bw;
+};
+
+__device__ __forceinline__ RoiGeom roi_geom(const float* roi, float ss, int PH, int PW) {
+    int sw = static_cast<int>(roundf(roi[1] * ss));
+    int sh = static_cast<int>(roundf(roi[2] * ss));
+    int ew = static_cast<int>(roundf(roi[3] * ss));
+    int eh = static_cast<int>(roundf(roi[4] * ss));
+    int rw = ew - sw + 1;
+    int rh = eh - sh + 1;
+    rw = rw > 1 ? rw : 1;
+    rh = rh > 1 ? rh : 1;
+    RoiGeom g;
+    g.sh = sh;
+    g.sw = sw;
+    g.bh = static_cast<float>(rh) / static_cast<float>(PH);
+    g.bw = static_cast<float>(rw) / static_cast<float>(PW);
+    return g;
+}
+
+__device__ __forceinline__ int4 geom_bin(const RoiGeom& g, int H, int W, int ph, int pw) {
+    int hs = static_cast<int>(floorf(static_cast<float>(ph) * g.bh)) + g.sh;
+    int ws = static_cast<int>(floorf(static_cast<float>(pw) * g.bw)) + g.sw;
+    int he = static_cast<int>(ceilf(static_cast<float>(ph + 1) * g.bh)) + g.sh;
+    int we = static_cast<int>(ceilf(static_cast<float>(pw + 1) * g.bw)) + g.sw;
+    return make_int4(min(max(hs, 0), H), min(max(he, 0), H), min(max(ws, 0), W),
+                     min(max(we, 0), W));
+}
+
+// Count of RoIs with batch index < b0 and < b1 (block-wide), for RoIs grouped by
+// non-decreasing batch index: image b's RoIs are then [count(<b), count(<b+1)).
+// `red` holds 2 ints per wave.
+template <int NT>
+__device__ __forceinline__ int2 roi_range_sorted(const float* __restrict__ rois, int R, int b0,
+                                                 int b1, int* red, int stride = 5) {
+    int c0 = 0, c1 = 0;
+    for (int r = threadIdx.x; r < R; r += NT) {
+        const int rb = static_cast<int>(rois[static_cast<size_t>(r) * stride]);
+        c0 += rb < b0;
+        c1 += rb < b1;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        c0 += __shfl_xor(c0, o, 64);
+        c1 += __shfl_xor(c1, o, 64);
+    }
+    const int wid = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        red[2 * wid] = c0;
+        red[2 * wid + 1] = c1;
+    }
+    __syncthreads();
+    int2 res = make_int2(0, 0);
+    for (int w = 0; w < NT / 64; ++w) {
+        res.x += red[2 * w];
+        res.y += red[2 * w + 1];
+    }
+    __syncthreads();  // red is reused by the caller
+    return res;
+}
+
+// The head's RoI transform + [idx, box] pack (nets/heads.py:42-47), fused into
+// the forward: `rois` are then [R,4] image-pixel boxes, `inds` their image index.
+struct HeadArgs {
+    const float* inds;
+    float img_h, img_w, fh, fw;
+    float* boxes;  // [R,5] written once (channel group 0) for the backward
+};
+
+__device__ __forceinline__ void head_box(const float* __restrict__ rois, const HeadArgs& hd, int r,
+                                         float (&bx)[5]) {
+    const float4 v = reinterpret_cast<const float4*>(rois)[r];
+    bx[0] = hd.inds[r];
+    bx[1] = v.x / hd.img_h * hd.fh;  // fp32 divide, then multiply (nets/heads.py:43-44)
+    bx[2] = v.y / hd.img_w * hd.fw;
+    bx[3] = v.z / hd.img_h * hd.fh;
+    bx[4] = v.w / hd.img_w * hd.fw;
+}
+
+// v_max3_f32 without the IEEE-mode canonicalisation the compiler adds around
+// fmaxf on loaded values: the tile holds no NaN (staged as -inf), and the sign
+// of a zero maximum is re-read from the tile after the scan.
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+    float d;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
+// Window class of a RoI: (max bin height, max bin width), each capped at 15;
+// the key orders the dense bin stream and the cost drives the balanced shares.
+__device__ __forceinline__ int2 geom_class(const RoiGeom& g, int H, int W, int PH, int PW) {
+    const int mh = min(min(static_cast<int>(ceilf(g.bh)) + 1, H), 15);
+    const int mw = min(min(static_cast<int>(ceilf(g.bw)) + 1, W), 15);
+    const int eh = g.sh + static_cast<int>(ceilf(g.bh * static_cast<float>(PH)));
+    const int ew = g.sw + static_cast<int>(ceilf(g.bw * static_cast<float>(PW)));
+    const bool outside = g.sh >= H || g.sw >= W || eh <= 0 || ew <= 0;
+    const int key = outside ? 0 : mh * 16 + mw;
+    const int cost = outside ? 2 : mh * ((mw + 1) >> 1) + 3;
+    return make_int2(key, cost);
+}
+
+// ------------------------------------------------------------- dense forward
+// Dynamic LDS (nothing static, the tile starts at offset 0):
+//   tile  NP planes x HWs float4: plane q = channels 4q..4q+3, pixel p at [q*HWs + p]
+//   geo   cap x int4 (sh, sw, bh bits, bw bits)   rid cap x int (RoI index)
+//   ord   cap x int (item order)                  key cap x u8 (window class)
+//   hist  256 x u32,  misc 64 x int
+// Grid (C/CG, split, N [+1 when !LIST: RoIs with an out-of-range batch index]):
+// the image index is slowest, so row N is dispatched after every real workgroup.
+// LIST: RoIs in any order, per-image lists from roi_lists_kernel; else RoIs
+// grouped by non-decreasing batch index (each workgroup finds its image's range).
+constexpr int kDenseMisc = 64;
+__host__ __device__ constexpr size_t dense_fixed_bytes() { return 256 * 4 + kDenseMisc * 4; }
+__host__ __device__ constexpr size_t dense_item_bytes() { return 16 + 4 + 4 + 1; }
+
+template <int NT, int CG, int FIX, bool HEAD, bool LIST>
+__global__ __launch_bounds__(NT) void roi_pool_fwd_dense_kernel(
+    const float* __restrict__ x, const float* __restrict__ rois, const int* __restrict__ list,
+    const int* __restrict__ cnt, int R, int C, int H, int W, int PH_, int PW_, float ss,
+    float* __restrict__ out, int32_t* __restrict__ argmax, int cap, HeadArgs hd) {
+    constexpr int NP = CG / 4;
+    constexpr int NW = NT / 64;
+    extern __shared__ __attribute__((aligned(16))) float4 q4[];
+    const int PH = FIX ? FIX : PH_, PW = FIX ? FIX : PW_;
+    const int PHW = PH * PW;
+    const int b = blockIdx.z;
+    const int c0 = blockIdx.x * CG;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int HW = H * W;
+    const int HWs = (HW + 15) & ~15;
+    const int split = gridDim.y, z = blockIdx.y;
+    int4* s_geo = reinterpret_cast<int4*>(q4 + NP * HWs);
+    int* s_rid = reinterpret_cast<int*>(s_geo + cap);
+    int* s_ord = s_rid + cap;
+    uint8_t* s_key = reinterpret_cast<uint8_t*>(s_ord + cap);
+    unsigned* s_hist = reinterpret_cast<unsigned*>(s_key + ((cap + 15) & ~15));
+    int* s_misc = reinterpret_cast<int*>(s_hist + 256);
+    auto load_box = [&](int r, float (&bx)[5]) {
+        if (HEAD) {
+            head_box(rois, hd, r, bx);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 5; ++j) bx[j] = rois[static_cast<size_t>(r) * 5 + j];
+        }
+    };
+
+    // ---- 0. the image's RoIs: [rbase, rbase + nr) or list[b][0, nr)
+    int rbase = 0, nr;
+    const int* lst = nullptr;
+    if (LIST) {
+        nr = cnt[b];
+        lst = list + static_cast<size_t>(b) * R;
+    } else {
+        const int N = gridDim.z - 1;
+        if (b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
+            const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, 0, N, s_misc, 1)
+                                 : roi_range_sorted<NT>(rois, R, 0, N, s_misc);
+            const int n_lo = rg.x, n_hi = R - rg.y, tot = n_lo + n_hi;
+            const int lo = static_cast<int>(static_cast<int64_t>(tot) * z / split);
+            const int hi = static_cast<int>(static_cast<int64_t>(tot) * (z + 1) / split);
+            if (HEAD && hd.boxes && blockIdx.x == 0)
+                for (int t = lo + tid; t < hi; t += NT) {
+                    const int r = t < n_lo ? t : rg.y + (t - n_lo);
+                    float bx[5];
+                    head_box(rois, hd, r, bx);
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
+                }
+            for (int e = lo * CG * PHW + tid; e < hi * CG * PHW; e += NT) {
+                const int t = e / (CG * PHW);
+                const int rem = e - t * (CG * PHW);
+                const int r = t < n_lo ? t : rg.y + (t - n_lo);
+                const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + rem;
+                out[o] = 0.0f;
+                argmax[o] = -1;
+            }
+            return;
+        }
+        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, b, b + 1, s_misc, 1)
+                             : roi_range_sorted<NT>(rois, R, b, b + 1, s_misc);
+        rbase = rg.x;
+        nr = rg.y - rg.x;
+    }
+    if (nr <= 0) return;
+    auto roi_of = [&](int t) { return LIST ? lst[t] : rbase + t; };
+    auto geom_of = [&](int r) {
+        float bx[5];
+        load_box(r, bx);
+        return roi_geom(bx, ss, PH, PW);
+    };
+
+    // ---- 1. cost-balanced share [lo, hi) of the image's RoIs (contiguous, by
+    // the cost midpoint of each RoI; every workgroup of the image computes the
+    // same cut, so the shares tile [0, nr) exactly)
+    int lo = 0, hi = nr;
+    if (split > 1) {
+        const int per = (nr + NT - 1) / NT;
+        const int t0 = min(tid * per, nr), t1 = min(t0 + per, nr);
+        int mine = 0;
+        for (int t = t0; t < t1; ++t) mine += geom_class(geom_of(roi_of(t)), H, W, PH, PW).y;
+        int incl = mine;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) s_misc[wid] = incl;
+        if (tid == 0) {
+            s_misc[32] = nr;
+            s_misc[33] = 0;
+        }
+        __syncthreads();
+        int64_t pre = incl - mine, total = 0;
+        for (int w = 0; w < NW; ++w) {
+            pre += w < wid ? s_misc[w] : 0;
+            total += s_misc[w];
+        }
+        for (int t = t0; t < t1; ++t) {
+            const int c = geom_class(geom_of(roi_of(t)), H, W, PH, PW).y;
+            int s = static_cast<int>(((2 * pre + c) * split) / (2 * total));
+            s = s < split - 1 ? s : split - 1;
+            if (s == z) {
+                atomicMin(&s_misc[32], t);
+                atomicMax(&s_misc[33], t + 1);
+            }
+            pre += c;
+        }
+        __syncthreads();
+        lo = s_misc[32];
+        hi = s_misc[33];
+        if (lo >= hi) return;  // uniform
+    }
+
+    // ---- 2. stage the CG planes (NaN -> -inf: never selected by the strict '>'
+    // against the -FLT_MAX start, and max3 never sees a NaN)
+    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+    for (int p = tid; p < HW; p += NT) {
+        float v[CG];
+#pragma unroll
+        for (int q = 0; q < CG; ++q) {
+            const float e = src[static_cast<size_t>(q) * HW + p];
+            v[q] = e != e ? -INFINITY : e;
+        }
+#pragma unroll
+        for (int k = 0; k < NP; ++k)
+            q4[k * HWs + p] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    }
+
+    const uint32_t plane_bytes = static_cast<uint32_t>(HWs) * 16u;
+    const char* tb = reinterpret_cast<const char*>(q4);
+    const uint32_t magic_phw = 0xFFFFFFFFu / static_cast<uint32_t>(PHW) + 1u;
+    const uint32_t magic_pw = 0xFFFFFFFFu / static_cast<uint32_t>(PW) + 1u;
+    // ---- 3. chunks of `cap` RoIs: geometry, order by window class, dense bins
+    for (int k0 = lo; k0 < hi; k0 += cap) {
+        const int cn = min(cap, hi - k0);
+        for (int i = tid; i < 256; i += NT) s_hist[i] = 0;
+        __syncthreads();  // tile staged / previous chunk done with geo, ord, hist
+        for (int i = tid; i < cn; i += NT) {
+            const int r = roi_of(k0 + i);
+            float bx[5];
+            load_box(r, bx);
+            if (HEAD && hd.boxes && blockIdx.x == 0) {
+#pragma unroll
+                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
+            }
+            const RoiGeom gm = roi_geom(bx, ss, PH, PW);
+            s_geo[i] = make_int4(gm.sh, gm.sw, __float_as_int(gm.bh), __float_as_int(gm.bw));
+            s_rid[i] = r;
+            const int key = geom_class(gm, H, W, PH, PW).x;
+            s_key[i] = static_cast<uint8_t>(key);
+            atomicAdd(&s_hist[255 - key], 1u);  // descending window class
+        }
+        __syncthreads();
+        if (wid == 0) {  // exclusive scan of the 256 buckets, 4 per lane
+            unsigned h[4], loc = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                h[j] = s_hist[4 * lane + j];
+                loc += h[j];
+            }
+            unsigned incl = loc;
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned v = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += v;
+            }
+            unsigned run = incl - loc;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                s_hist[4 * lane + j] = run;
+                run += h[j];
+            }
+        }
+        if (tid == 0) s_misc[40] = 0;
+        __syncthreads();
+        for (int i = tid; i < cn; i += NT) s_ord[atomicAdd(&s_hist[255 - s_key[i]], 1u)] = i;
+        __syncthreads();
+
+        const int total = cn * PHW;
+        int f0 = 0;
+        if (lane == 0) f0 = atomicAdd(&s_misc[40], 64);
+        f0 = __builtin_amdgcn_readfirstlane(f0);
+        while (f0 < total) {
+            int fn = 0;
+            if (lane == 0) fn = atomicAdd(&s_misc[40], 64);  // prefetch the next chunk
+            const int f = f0 + lane;
+            const bool live = f < total;
+            // (the magic reciprocal of 1 wraps to 0: divisors of 1 bypass it)
+            const int t = FIX ? (live ? f / PHW : 0)
+                              : (live ? (PHW == 1 ? f : static_cast<int>(__umulhi(static_cast<uint32_t>(f), magic_phw)))
+                                      : 0);
+            const int k = f - t * PHW;
+            const int ph = FIX ? k / PW
+                               : (PW == 1 ? k : static_cast<int>(__umulhi(static_cast<uint32_t>(k), magic_pw)));
+            const int pw = k - ph * PW;
+            const int item = s_ord[t];
+            const int4 gq = s_geo[item];
+            RoiGeom gm;
+            gm.sh = gq.x;
+            gm.sw = gq.y;
+            gm.bh = __int_as_float(gq.z);
+            gm.bw = __int_as_float(gq.w);
+            int4 g = geom_bin(gm, H, W, ph, pw);
+            if (!live) g = make_int4(0, 0, 0, 0);
+            const bool empty = g.y <= g.x || g.w <= g.z;
+            float mv[CG];
+            int mi[CG];  // LDS byte offset of the max's pixel in plane 0 (-16: none)
+#pragma unroll
+            for (int c = 0; c < CG; ++c) {
+                mv[c] = empty ? 0.0f : -FLT_MAX;
+                mi[c] = -16;
+            }
+            // One pixel pair (a, b) in row-major order: per channel m' = max3(m, a, b);
+            // the index moves iff m' > m, to a if a == m' (a comes first).  A pair
+            // past the window's row end repeats its last pixel, which can never
+            // pass the strict '>' again.  src -> dst are different registers; the
+            // loop takes two pairs per trip (mv -> m2 -> mv), so the running
+            // maxima need no copy back except after an odd pair at a row end.
+            float m2[CG];
+            auto pair = [&](const float (&src)[CG], float (&dst)[CG], int ia, int ib) {
+                float4 va[NP], vb[NP];
+#pragma unroll
+                for (int q = 0; q < NP; ++q) {
+                    va[q] = *static_cast<const float4*>(
+                        __builtin_assume_aligned(tb + q * plane_bytes + ia, 16));
+                    vb[q] = *static_cast<const float4*>(
+                        __builtin_assume_aligned(tb + q * plane_bytes + ib, 16));
+                }
+#pragma unroll
+                for (int q = 0; q < NP; ++q) {
+                    const float a4[4] = {va[q].x, va[q].y, va[q].z, va[q].w};
+                    const float b4[4] = {vb[q].x, vb[q].y, vb[q].z, vb[q].w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int c = 4 * q + j;
+                        const float m = max3_raw(src[c], a4[j], b4[j]);
+                        const int ip = a4[j] == m ? ia : ib;
+                        mi[c] = m > src[c] ? ip : mi[c];
+                        dst[c] = m;
+                    }
+                }
+            };
+            const int wl = g.w - 1;
+            for (int h = g.x; h < g.y; ++h) {
+                const int rb = h * W;
+                int w = g.z;
+                for (; w + 2 < g.w; w += 4) {  // >= 3 pixels left: two pairs
+                    pair(mv, m2, (rb + w) << 4, (rb + w + 1) << 4);
+                    pair(m2, mv, (rb + w + 2) << 4, (rb + min(w + 3, wl)) << 4);
+                }
+                if (w < g.w) {  // 1 or 2 pixels left
+                    pair(mv, m2, (rb + w) << 4, (rb + min(w + 1, wl)) << 4);
+#pragma unroll
+                    for (int c = 0; c < CG; ++c) mv[c] = m2[c];
+                }
+            }
+            if (live) {
+                const int r = s_rid[item];
+                const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + k;
+#pragma unroll
+                for (int c = 0; c < CG; ++c) {
+                    const int idx = mi[c] >> 4;
+                    float v = mv[c];
+                    if (v == 0.0f && idx >= 0)  // exact bits (sign) of a zero maximum
+                        v = reinterpret_cast<const float*>(tb + (c >> 2) * plane_bytes)[idx * 4 + (c & 3)];
+                    out[o + static_cast<size_t>(c) * PHW] = v;
+                    argmax[o + static_cast<size_t>(c) * PHW] = idx;
+                }
+            }
+            f0 = __builtin_amdgcn_readfirstlane(fn);
+        }
+    }
+}
+
+// Timeline probe of the wave-per-RoI forward (instrumented builds only,
+// -DFRCNN_POOL_PROF, tools/probe_pool.py): per workgroup the realtime clock
+// (100 MHz) at entry, after the RoI range, after the tile is staged, and the
+// last wave's exit; plus the RoIs it pooled.
+#ifdef FRCNN_POOL_PROF
+constexpr int kPoolProfSlots = 8192;
+__device__ unsigned long long g_pool_prof[kPoolProfSlots][4];
+__device__ unsigned int g_pool_prof_rois[kPoolProfSlots];
+#define PPROF_T(k)                                                                                  \
+    do {                                                                                            \
+        const unsigned long long _t = __builtin_amdgcn_s_memrealtime();                             \
+        const unsigned _wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);         \
+        if (_wg < kPoolProfSlots) {                                                                 \
+            if ((k) == 3) {                                                                         \
+                if ((threadIdx.x & 63) == 0) atomicMax(&g_pool_prof[_wg][3], _t);                   \
+            } else if (threadIdx.x == 0) {                                                          \
+                g_pool_prof[_wg][k] = _t;                                                           \
+            }                                                                                       \
+        }                                                                                           \
+    } while (0)
+#define PPROF_ROIS(n)                                                                               \
+    do {                                                                                            \
+        const unsigned _wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);         \
+        if (_wg < kPoolProfSlots && threadIdx.x == 0) g_pool_prof_rois[_wg] = (n);                  \
+    } while (0)
+#else
+#define PPROF_T(k) do {} while (0)
+#define PPROF_ROIS(n) do {} while (0)
+#endif
+
+// Tile layout of the wave-per-RoI forward: 16-pixel groups, the group's NP
+// 4-channel planes back to back (pixel p of plane q at float4
+// (g*NP + q)*16 + s, g = p >> 4), the slot s = (p ^ g) & 15 XOR-swizzled so
+// that a ds_read_b128 of bins a bin width apart does not collide, and the
+// planes of one pixel 256 B apart -- LDS immediate offsets.
+template <int NP>
+__device__ __forceinline__ const float4* tile_px(const float4* q4, int p) {
+    const int g = p >> 4;
+    return q4 + g * (NP * 16) + ((p ^ g) & 15);
+}
+
+// ------------------------------------------------- wave-per-RoI forward
+// The default forward for RoIs grouped by image.  Work = (image, CG-channel
+// group) "pairs" p = b*G + g (G = C/CG; pair b = N holds the RoIs whose batch
+// index is outside [0, N)).  The grid is persistent: one 1024-thread
+// workgroup per resident slot of the CUs the launch stream may use.  A
+// workgroup stages its pair's CG channel planes once into LDS (tile_px layout)
+// and its 16 waves pull the pair's RoIs one at a time from a global counter
+// (sched[p], zeroed before the launch), so every workgroup on a pair finishes
+// together whatever the RoI sizes or the speed of its CU.  When its pair is
+// drained it takes the pair with the most RoIs left (restaging that tile): a
+// pair nobody started (more pairs than workgroups, the out-of-range pair) at
+// any count, a started one only with >= kStealMin left (a restage costs about
+// as much as that many RoIs).  Any CU count works -- the pool can run beside
+// the proposal kernels on a CU-masked stream.
+// Per RoI: one wave, lane = bin: each lane walks its window once and updates
+// CG (max, first index) pairs with torchvision's strict '>' -- the RoI
+// geometry, the window walk and the pixel address are shared by CG channels;
+// per channel the 49 lanes write one contiguous 196-B run.  The next RoI's
+// index is pulled and its box loaded while the current one is pooled.
+// HEAD: fused with the head's RoI transform (nets/heads.py:42-47): `rois` are
+// the [R,4] image boxes, hd.inds their image index; the [idx, box] rows are
+// formed in registers and (channel group 0) written to hd.boxes.
+// (Measured alternatives -- RoI bins packed 64 per wave, bins sorted by window
+// shape per image or per RoI block, pixel-pair max3 scans -- are slower:
+// DESIGN.md §3, profiles/r2_experiments.md.)
+constexpr int kStealMin = 48;   // RoIs a started pair must have left to be taken over
+constexpr int kChunk = 16;      // RoIs per claim on a pair's global counter
+constexpr int kRing = 64;       // LDS ring of claimed RoI offsets (>= 3 chunks)
+
+template <int NT, int CG, bool HEAD>
+__global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
+    const float* __restrict__ x, const float* __restrict__ rois, int R, int N, int C, int H, int W, int PH,
+    int PW, float ss, float* __restrict__ out, int32_t* __restrict__ argmax, int* __restrict__ sched,
+    HeadArgs hd) {
+    constexpr int NP = CG / 4;
+    constexpr int NW = NT / 64;
+    extern __shared__ __attribute__((aligned(16))) float4 q4[];  // tile; then s_bnd[N + 1]
+    __shared__ int s_pick[2 * NW];
+    __shared__ int s_ring[kRing];
+    __shared__ int s_taken, s_pub, s_done;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int HW = H * W;
+    const int HWs = (HW + 15) & ~15;
+    const int PHW = PH * PW;
+    const int G = C / CG;
+    const int P = (N + 1) * G;
+    const int Preal = N * G;
+    int* s_bnd = reinterpret_cast<int*>(q4 + NP * HWs);  // [0..N]: #RoIs with batch index < b
+    PPROF_T(0);
+    // ---- image boundaries of the sorted RoIs: every RoI whose batch index
+    // differs from its predecessor's writes the boundaries in between
+    {
+        const float* bi = HEAD ? hd.inds : rois;
+        const int stride = HEAD ? 1 : 5;
+        auto cl = [&](float v) {  // batch index clamped to [-1, N]
+            const int i = static_cast<int>(v);
+            return i < 0 ? -1 : (i > N ? N : i);
+        };
+        for (int r = tid; r <= R; r += NT) {
+            const int cur = r < R ? cl(bi[static_cast<size_t>(r) * stride]) : N + 1;
+            const int prev = r > 0 ? cl(bi[static_cast<size_t>(r - 1) * stride]) : -1;
+            for (int bb = max(prev + 1, 0); bb <= min(cur, N); ++bb) s_bnd[bb] = r;
+        }
+    }
+    __syncthreads();
+    PPROF_T(1);
+    auto nr_of = [&](int p) {
+        const int b = p / G;
+        return b < N ? s_bnd[b + 1] - s_bnd[b] : s_bnd[0] + (R - s_bnd[N]);
+    };
+    // claim the next chunk of pair p into the ring (one thread)
+    auto claim = [&](int p, int nr) {
+        const int g0 = atomicAdd(&sched[p], kChunk);
+        const int n = g0 >= nr ? 0 : min(kChunk, nr - g0);
+        const int at = __hip_atomic_load(&s_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (int i = 0; i < n; ++i) s_ring[(at + i) % kRing] = g0 + i;
+        if (n < kChunk) __hip_atomic_store(&s_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): ring entries land before the count
+        __hip_atomic_fetch_add(&s_pub, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    const int ph = lane / PW, pw = lane - (lane / PW) * PW;
+    const bool act = lane < PHW;
+    int p = Preal > 0 ? static_cast<int>(blockIdx.x) % Preal : -1;
+    int nstage = 0;
+    while (p >= 0) {
+        const int b = p / G;
+        const int c0 = (p - b * G) * CG;
+        const int nr = nr_of(p);
+        const int lo = b < N ? s_bnd[b] : 0, gap = b < N ? 0 : s_bnd[N] - s_bnd[0];
+        auto roi_of = [&](int t) { return (b < N || t < s_bnd[0]) ? lo + t : t + gap; };
+        if (tid == 0) {
+            s_taken = 0;
+            s_pub = 0;
+            s_done = 0;
+            claim(p, nr);
+            if (!s_done) claim(p, nr);
+        }
+        if (b < N && nr > 0) {  // stage the pair's CG planes
+            const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+            for (int px = tid; px < HW; px += NT) {
+                float v[CG];
+#pragma unroll
+                for (int q = 0; q < CG; ++q) v[q] = src[static_cast<size_t>(q) * HW + px];
+                float4* pp = const_cast<float4*>(tile_px<NP>(q4, px));
+#pragma unroll
+                for (int k = 0; k < NP; ++k) pp[16 * k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+            }
+            ++nstage;
+        }
+        __syncthreads();
+        if (nstage == 1) PPROF_T(2);
+        // next RoI offset of this workgroup (-1: the pair is drained); the wave
+        // that enters a new chunk claims the one after it
+        auto take = [&]() {
+            int t = -1;
+            if (lane == 0) {
+                const int i = __hip_atomic_fetch_add(&s_taken, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                while (true) {
+                    const int pub = __hip_atomic_load(&s_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (i < pub) {
+                        t = __hip_atomic_load(&s_ring[i % kRing], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        break;
+                    }
+                    if (__hip_atomic_load(&s_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
+                        i >= __hip_atomic_load(&s_pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+                        break;
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                if (t >= 0 && i >= kChunk && i % kChunk == 0 &&
+                    !__hip_atomic_load(&s_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+                    claim(p, nr);
+            }
+            return __builtin_amdgcn_readfirstlane(t);
+        };
+        auto load_box = [&](int t, float (&bx)[5]) {
+            const int r = roi_of(t);
+            if (HEAD) {
+                head_box(rois, hd, r, bx);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 5; ++j) bx[j] = rois[static_cast<size_t>(r) * 5 + j];
+            }
+        };
+        int t = take();
+        float bx[5];
+        if (t >= 0) load_box(t, bx);
+        while (t >= 0) {
+            const int tn = take();
+            float bn[5];
+            if (tn >= 0) load_box(tn, bn);  // in flight while RoI t is pooled
+            const int r = roi_of(t);
+            if (HEAD && hd.boxes && c0 == 0 && lane == 0) {
+#pragma unroll
+                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
+            }
+            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
+            if (b == N) {  // batch index outside [0, N): 0 / -1 (torchvision: UB)
+                if (act) {
+#pragma unroll
+                    for (int c = 0; c < CG; ++c) {
+                        out[o + static_cast<size_t>(c) * PHW] = 0.0f;
+                        argmax[o + static_cast<size_t>(c) * PHW] = -1;
+                    }
+                }
+            } else {
+                const RoiGeom gm = roi_geom(bx, ss, PH, PW);
+                int4 g = geom_bin(gm, H, W, ph, pw);
+                if (!act) g = make_int4(0, 0, 0, 0);
+                const bool empty = g.y <= g.x || g.w <= g.z;
+                float mv[CG];
+                int mi[CG];
+#pragma unroll
+                for (int c = 0; c < CG; ++c) {
+                    mv[c] = empty ? 0.0f : -FLT_MAX;
+                    mi[c] = -1;
+                }
+                for (int h = g.x; h < g.y; ++h) {
+                    const int rb = h * W;
+                    for (int w = g.z; w < g.w; ++w) {
+                        const int ii = rb + w;
+                        const float4* pp = tile_px<NP>(q4, ii);
+                        float4 v[NP];
+#pragma unroll
+                        for (int q = 0; q < NP; ++q) v[q] = pp[16 * q];
+                        // all NP reads in flight before the first compare (else the compiler
+                        // waits on each read in turn: NP LDS round trips per pixel)
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int q = 0; q < NP; ++q) {
+                            const float vv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                if (vv[j] > mv[4 * q + j]) {  // torchvision's strict '>'
+                                    mv[4 * q + j] = vv[j];
+                                    mi[4 * q + j] = ii;
+                                }
+                            }
+                        }
+                    }
+                }
+                if (act) {
+#pragma unroll
+                    for (int c = 0; c < CG; ++c) {
+                        out[o + static_cast<size_t>(c) * PHW] = mv[c];
+                        argmax[o + static_cast<size_t>(c) * PHW] = mi[c];
+                    }
+                }
+            }
+            t = tn;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) bx[j] = bn[j];
+        }
+        __syncthreads();  // every wave is done with the tile and the ring
+        // ---- next pair: the most RoIs left (a pair no workgroup started at any count)
+        int best = 0, bp = -1;
+        for (int q = tid; q < P; q += NT) {
+            const int left = nr_of(q) - __hip_atomic_load(&sched[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool owned = q < Preal && q < static_cast<int>(gridDim.x);
+            if (left > best && (left >= kStealMin || !owned)) {
+                best = left;
+                bp = q;
+            }
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const int ob = __shfl_xor(best, o, 64), op = __shfl_xor(bp, o, 64);
+            if (ob > best || (ob == best && op > bp)) {
+                best = ob;
+                bp = op;
+            }
+        }
+        if (lane == 0) {
+            s_pick[2 * wid] = best;
+            s_pick[2 * wid + 1] = bp;
+        }
+        __syncthreads();
+        best = 0;
+        bp = -1;
+        for (int w2 = 0; w2 < NW; ++w2) {
+            if (s_pick[2 * w2] > best || (s_pick[2 * w2] == best && s_pick[2 * w2 + 1] > bp)) {
+                best = s_pick[2 * w2];
+                bp = s_pick[2 * w2 + 1];
+            }
+        }
+        __syncthreads();  // s_pick is rewritten by the next pick
+        p = best > 0 ? bp : -1;
+    }
+    PPROF_T(3);
+}
+
+// nets/heads.py:42-47 (fp32 divide, then multiply) + [idx, box] pack.
+__global__ __launch_bounds__(256) void roi_transform_kernel(const float* __restrict__ rois,
+                                                            const float* __restrict__ inds,
+                                                            int64_t R, float img_h, float img_w,
+                                                            float fh, float fw,
+                                                            float* __restrict__ boxes) {
+    int64_t r = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    if (r >= R) return;
+    float4 v = reinterpret_cast<const float4*>(rois)[r];
+    float* o = boxes + r * 5;
+    o[0] = inds[r];
+    o[1] = v.x / img_h * fh;
+    o[2] = v.y / img_w * fw;
+    o[3] = v.z / img_h * fh;
+    o[4] = v.w / img_w * fw;
+}
+
+// Ordered per-image RoI lists: list[b][*] = RoIs with batch index b, ascending.
+// Block N (the extra one) collects the RoIs whose batch index is outside [0, N).
+// `stride`: floats between consecutive batch indices (5 for [R,5] RoIs, 1 for
+// the head's roi_inds).
+__global__ __launch_bounds__(1024) void roi_lists_kernel(const float* __restrict__ rois, int R,
+                                                         int N, int* __restrict__ list,
+                                                         int* __restrict__ cnt, int stride = 5) {
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    __shared__ int s_w[16];
+    int base = 0;
+    for (int r0 = 0; r0 < R; r0 += 1024) {
+        int r = r0 + tid;
+        int rb = r < R ? static_cast<int>(rois[static_cast<size_t>(r) * stride]) : -1;
+        bool m = r < R && (b < N ? rb == b : (rb < 0 || rb >= N));
+        uint64_t bal = __ballot(m);
+        if (lane == 0) s_w[wid] = __popcll(bal);
+        __syncthreads();
+        int before = 0, tot = 0;
+        for (int w = 0; w < 16; ++w) {
+            before += w < wid ? s_w[w] : 0;
+            tot += s_w[w];
+        }
+        if (m) list[static_cast<size_t>(b) * R + base + before + __popcll(bal & lanemask_lt())] = r;
+        base += tot;
+        __syncthreads();
+    }
+    if (tid == 0) cnt[b] = base;
+}
+
+// Outputs of RoIs with an out-of-range batch index: 0 / -1 (torchvision: UB);
+// with a head transform (hd.inds) also their [idx, box] rows.
+__global__ __launch_bounds__(256) void roi_pool_invalid_fill_kernel(const int* __restrict__ list,
+                                                                    const int* __restrict__ cnt,
+                                                                    int R, int N, size_t per_roi,
+                                                                    float* __restrict__ out,
+                                                                    int32_t* __restrict__ argmax,
+                                                                    const float* __restrict__ rois4 = nullptr,
+                                                                    HeadArgs hd = HeadArgs{}) {
+    const int n = cnt[N];
+    for (int t = blockIdx.x; t < n; t += gridDim.x) {
+        const int r = list[static_cast<size_t>(N) * R + t];
+        const size_t base = static_cast<size_t>(r) * per_roi;
+        if (hd.inds && threadIdx.x == 0) {
+            float bx[5];
+            head_box(rois4, hd, r, bx);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
+        }
+        for (size_t e = threadIdx.x; e < per_roi; e += 256) {
+            out[base + e] = 0.0f;
+            argmax[base + e] = -1;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ backward
+// Per RoI and bin k: mask of the earlier bins of the same 64-bin chunk whose
+// (non-empty) windows overlap bin k's -- the only bins that can share its
+// argmax pixel.
+// With PH*PW <= 64 it also writes code[r][k]: which of bin k's earlier grid
+// neighbours overlap it (1 left, 2 up, 4 up-left, 8 up-right) and, in bit 4,
+// whether ANY bin of the RoI has an overlap outside that set (the RoI then
+// takes the general mask walk in the ring kernel).
+__global__ __launch_bounds__(256) void roi_bwd_prep_kernel(const float* __restrict__ rois, int H,
+                                                           int W, int PH, int PW, float ss,
+                                                           uint64_t* __restrict__ cmask,
+                                                           uint8_t* __restrict__ code) {
+    __shared__ int4 bins[kMaxBins];
+    const int r = blockIdx.x;
+    const int PHW = PH * PW;
+    const float* roi = rois + static_cast<size_t>(r) * 5;
+    for (int k = threadIdx.x; k < PHW; k += 256)
+        bins[k] = roi_bin(roi, ss, H, W, PH, PW, k / PW, k % PW);
+    __syncthreads();
+    for (int k = threadIdx.x; k < PHW; k += 256) {
+        int4 g = bins[k];
+        uint64_t m = 0;
+        bool ne = g.y > g.x && g.w > g.z;
+        int k0 = k & ~63;
+        for (int p = k0; ne && p < k; ++p) {
+            int4 q = bins[p];
+            bool ov = q.y > q.x && q.w > q.z && q.x < g.y && g.x < q.y && q.z < g.w && g.z < q.w;
+            if (ov) m |= 1ull << (p - k0);
+        }
+        cmask[static_cast<size_t>(r) * PHW + k] = m;
+    }
+    if (code == nullptr || PHW > 64) return;  // uniform
+    const int k = threadIdx.x;
+    uint32_t nb = 0;
+    bool other = false;
+    if (k < PHW) {
+        const uint64_t m = cmask[static_cast<size_t>(r) * PHW + k];  // this thread's own write
+        const int pw = k % PW;
+        uint64_t known = 0;
+        if (pw > 0) {
+            known |= 1ull << (k - 1);
+            nb |= (m >> (k - 1)) & 1u;
+        }
+        if (k >= PW) {
+            known |= 1ull << (k - PW);
+            nb |= ((m >> (k - PW)) & 1u) << 1;
+            if (pw > 0) {
+                known |= 1ull << (k - PW - 1);
+                nb |= ((m >> (k - PW - 1)) & 1u) << 2;
+            }
+            if (pw < PW - 1) {
+                known |= 1ull << (k - PW + 1);
+                nb |= ((m >> (k - PW + 1)) & 1u) << 3;
+            }
+        }
+        other = (m & ~known) != 0;
+    }
+    const int slow = __syncthreads_or(other);
+    if (k < PHW) code[static_cast<size_t>(r) * PHW + k] = static_cast<uint8_t>(nb | (slow ? 16u : 0u));
+}
+
+// General plane-owner backward (any output size; planes in LDS or, when a
+// plane does not fit, in grad_in itself with agent-scope load/store rounds).
+template <bool IN_LDS>
+__global__ void roi_pool_bwd_kernel(const float* __restrict__ grad,
+                                    const int32_t* __restrict__ argmax,
+                                    const uint64_t* __restrict__ cmask,
+                                    const int* __restrict__ list, const int* __restrict__ cnt,
+                                    int R, int C, int HW, int PHW, int CPW,
+                                    float* __restrict__ grad_in) {
+    extern __shared__ __attribute__((aligned(16))) float planes[];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int b = blockIdx.y;
+    const int c = blockIdx.x * CPW + wid;
+    if (c >= C) return;  // whole wave; no workgroup barrier below
+    float* gplane = grad_in + (static_cast<size_t>(b) * C + c) * HW;
+    float* plane = IN_LDS ? planes + static_cast<size_t>(wid) * HW : gplane;
+    for (int i = lane; i < HW; i += 64) {
+        if (IN_LDS) plane[i] = 0.0f;
+        else __hip_atomic_store(plane + i, 0.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!IN_LDS) __builtin_amdgcn_s_waitcnt(0);
+    const int nr = cnt[b];
+    const int* lst = list + static_cast<size_t>(b) * R;
+    for (int t = 0; t < nr; ++t) {
+        const int n = __builtin_amdgcn_readfirstlane(lst[t]);
+        const size_t base = (static_cast<size_t>(n) * C + c) * PHW;
+        for (int k0 = 0; k0 < PHW; k0 += 64) {
+            const int k = k0 + lane;
+            const bool act = k < PHW;
+            const int am = act ? argmax[base + k] : -1;
+            const float g = act ? grad[base + k] : 0.0f;
+            uint64_t pend = (act && am != -1) ? cmask[static_cast<size_t>(n) * PHW + k] : 0ull;
+            int depth = 0;
+            while (__ballot(pend != 0)) {
+                int p = pend ? __ffsll(static_cast<unsigned long long>(pend)) - 1 : lane;
+                pend &= pend - 1;
+                int amp = __shfl(am, p, 64);
+                if (p != lane && amp == am) ++depth;
+            }
+            int dmax = (am != -1) ? depth : -1;
+            for (int o = 32; o > 0; o >>= 1) dmax = max(dmax, __shfl_xor(dmax, o, 64));
+            for (int d = 0; d <= dmax; ++d) {
+                if (am != -1 && depth == d) {
+                    if (IN_LDS) {
+                        plane[am] += g;
+                    } else {
+                        float cur = __hip_atomic_load(plane + am, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(plane + am, cur + g, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+                // Round boundary: this round's plane writes land before the next
+                // round's reads (other lanes, same pixel).  Also a compiler barrier.
+                if (IN_LDS) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                else __builtin_amdgcn_s_waitcnt(0);
+            }
+        }
+    }
+    if (IN_LDS) {
+        if ((HW & 3) == 0) {
+            const float4* s4 = reinterpret_cast<const float4*>(plane);
+            float4* d4 = reinterpret_cast<float4*>(gplane);
+            for (int i = lane; i < HW / 4; i += 64) d4[i] = s4[i];
+        } else {
+            for (int i = lane; i < HW; i += 64) gplane[i] = plane[i];
+        }
+    }
+}
+
+// Same plane-owner backward for PH*PW <= 64 (one bin per lane, the 7x7 head),
+// latency-hidden: the loads of RoI t+D are issued before RoI t is applied (a
+// D-deep register ring, slot index static after unrolling), and the RoI
+// indices come by scalar loads, so no vector load sits between the ring's loads
+// in the in-order vmcnt queue.  Summation order per pixel is unchanged (RoIs
+// ascending, bins ascending within a RoI): bit-identical results.
+template <int D>
+__global__ __launch_bounds__(1024) void roi_pool_bwd_pf_kernel(
+    const float* __restrict__ grad, const int32_t* __restrict__ argmax,
+    const uint64_t* __restrict__ cmask, const uint8_t* __restrict__ code,
+    const int* __restrict__ list, const int* __restrict__ cnt,
+    int R, int C, int HW, int PHW, int PW, int CPW, float* __restrict__ grad_in) {
+    extern __shared__ __attribute__((aligned(16))) float planes[];
+    const int lane = threadIdx.x & 63;
+    // wave-uniform in an SGPR: the per-RoI grad / argmax bases are then scalar,
+    // and each lane's load is base (SGPR) + its bin offset (VGPR, fixed)
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = blockIdx.y;
+    const int c = blockIdx.x * CPW + wid;
+    if (c >= C) return;  // whole wave; no workgroup barrier below
+    float* gplane = grad_in + (static_cast<size_t>(b) * C + c) * HW;
+    float* plane = planes + static_cast<size_t>(wid) * HW;
+    for (int i = lane; i < HW; i += 64) plane[i] = 0.0f;
+    const int nr = cnt[b];
+    // Grid neighbours that come earlier in bin order: left, up-left, up,
+    // up-right.  When every overlap of a RoI is among them (bins >= 1 pixel:
+    // windows only share their floor/ceil border row / column), a bin's rank
+    // among the bins with the same argmax pixel takes four fixed-lane reads
+    // instead of a walk over its overlap mask.
+    const int pw_i = lane % PW;
+    const bool has_l = pw_i > 0, has_u = lane >= PW;
+    const bool has_r = pw_i < PW - 1;
+    const int n_l = has_l ? lane - 1 : lane, n_u = has_u ? lane - PW : lane;
+    const int n_ul = (has_u && has_l) ? lane - PW - 1 : lane;
+    const int n_ur = (has_u && has_r) ? lane - PW + 1 : lane;
+    if (nr > 0) {
+        const int* lst = list + static_cast<size_t>(b) * R;  // wave-uniform: scalar loads
+        const bool act = lane < PHW;
+        // Loads are unconditional (idle lanes re-read bin 0, RoIs past the end
+        // re-read the last one): a conditional load makes the compiler wait
+        // for the whole vmcnt queue at the branch join, which undoes the ring.
+        const int kl = act ? lane : 0;
+        int am_r[D];
+        float g_r[D];
+        uint32_t cd_r[D];
+        uint64_t cm_r[D];  // full overlap mask, used only by RoIs flagged slow
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int n = lst[d < nr ? d : nr - 1];
+            const size_t base = (static_cast<size_t>(n) * C + c) * PHW;
+            const size_t nb = static_cast<size_t>(n) * PHW;
+            am_r[d] = (argmax + base)[kl];
+            g_r[d] = (grad + base)[kl];
+            cd_r[d] = (code + nb)[kl];
+            cm_r[d] = (cmask + nb)[kl];
+            // keep the loop's issue order (slot by slot): the waitcnt pass then
+            // merges identical queues at the loop header instead of draining
+            asm volatile("" ::: "memory");
+        }
+        for (int t0 = 0; t0 < nr; t0 += D) {
+            // RoI indices of this group's refills (scalar loads: lgkmcnt, not
+            // in the vector-load queue)
+            int nx[D];
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const int tn = t0 + D + d;
+                nx[d] = lst[tn < nr ? tn : nr - 1];
+            }
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                // no early exit for the tail: a break would give the loop a
+                // second path into its header with another load order, and the
+                // waitcnt pass would drain the queue there every group
+                const bool live = t0 + d < nr;
+                // Take slot d's values into fresh registers (asm copies the
+                // compiler cannot coalesce away) so the refill lands in the
+                // slot's own registers: no back-edge copy, no wait on it.
+                int am;
+                float g;
+                uint32_t cd;
+                asm volatile("v_mov_b32 %0, %1" : "=v"(am) : "v"(am_r[d]));
+                asm volatile("v_mov_b32 %0, %1" : "=v"(g) : "v"(g_r[d]));
+                asm volatile("v_mov_b32 %0, %1" : "=v"(cd) : "v"(cd_r[d]));
+                uint32_t cm_lo, cm_hi;
+                asm volatile("v_mov_b32 %0, %1" : "=v"(cm_lo) : "v"(static_cast<uint32_t>(cm_r[d])));
+                asm volatile("v_mov_b32 %0, %1" : "=v"(cm_hi) : "v"(static_cast<uint32_t>(cm_r[d] >> 32)));
+                if (!live || !act) am = -1;
+                {  // refill this slot with RoI t + D before applying RoI t
+                    const int n = nx[d];
+                    const size_t base = (static_cast<size_t>(n) * C + c) * PHW;
+                    const size_t nb = static_cast<size_t>(n) * PHW;
+                    am_r[d] = (argmax + base)[kl];
+                    g_r[d] = (grad + base)[kl];
+                    cd_r[d] = (code + nb)[kl];
+                    cm_r[d] = (cmask + nb)[kl];
+                }
+                // depth = rank of this bin among the RoI's bins with the same
+                // argmax pixel (those windows all contain the pixel, so they
+                // overlap: candidates are the bits of the overlap mask)
+                int depth = 0;
+                if ((__builtin_amdgcn_readfirstlane(cd) & 16) == 0) {  // bin 0's code: the RoI flag
+                    const int a_l = __builtin_amdgcn_ds_bpermute(n_l << 2, am);
+                    const int a_u = __builtin_amdgcn_ds_bpermute(n_u << 2, am);
+                    const int a_ul = __builtin_amdgcn_ds_bpermute(n_ul << 2, am);
+                    const int a_ur = __builtin_amdgcn_ds_bpermute(n_ur << 2, am);
+                    depth = ((cd & 1) && a_l == am) + ((cd & 2) && a_u == am) +
+                            ((cd & 4) && a_ul == am) + ((cd & 8) && a_ur == am);
+                } else {  // overlaps beyond the grid neighbours: walk the full mask
+                    uint64_t pend = am != -1 ? ((static_cast<uint64_t>(cm_hi) << 32) | cm_lo) : 0ull;
+                    while (__ballot(pend != 0)) {
+                        const int p = pend ? __ffsll(static_cast<unsigned long long>(pend)) - 1 : lane;
+                        pend &= pend - 1;
+                        const int amp = __builtin_amdgcn_ds_bpermute(p << 2, am);
+                        if (p != lane && amp == am) ++depth;
+                    }
+                }
+                // apply in rank order; ranks are unique per pixel, so a round's
+                // read-add-write touches distinct pixels.  LDS executes a wave's
+                // instructions in issue order, so round r+1's reads see round
+                // r's writes without a wait (the asm is only a compiler
+                // barrier).  ds_add_f32 is exact too, but measured 1.4x slower.
+                for (int r = 0;; ++r) {
+                    if (am != -1 && depth == r) plane[am] += g;
+                    asm volatile("" ::: "memory");
+                    if (__ballot(am != -1 && depth > r) == 0) break;
+                }
+            }
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if ((HW & 3) == 0) {
+        const float4* s4 = reinterpret_cast<const float4*>(plane);
+        float4* d4 = reinterpret_cast<float4*>(gplane);
+        for (int i = lane; i < HW / 4; i += 64) d4[i] = s4[i];
+    } else {
+        for (int i = lane; i < HW; i += 64) gplane[i] = plane[i];
+    }
+}
+
+}  // namespace frcnn
+
+using namespace frcnn;
+
+extern "C" int frcnn_roi_transform(const float* rois, const float* roi_inds, int64_t R, float img_h,
+                                   float img_w, int feat_h, int feat_w, float* boxes,
+                                   void* stream) {
+    FRCNN_REQUIRE(R >= 0, "frcnn_roi_transform: R < 0");
+    if (R == 0) return FRCNN_OK;
+    FRCNN_REQUIRE(rois && roi_inds && boxes, "frcnn_roi_transform: null pointer");
+    hipLaunchKernelGGL(roi_transform_kernel, dim3(static_cast<unsigned>((R + 255) / 256)),
+                       dim3(256), 0, as_stream(stream), rois, roi_inds, R, img_h, img_w,
+                       static_cast<float>(feat_h), static_cast<float>(feat_w), boxes);
+    FRCNN_LAUNCH_CHECK("roi_transform_kernel");
+    return FRCNN_OK;
+}
+
+#ifdef FRCNN_POOL_PROF
+extern "C" int frcnn_debug_pool_prof(unsigned long long* times, unsigned* rois, int reset) {
+    (void)hipMemcpyFromSymbol(times, HIP_SYMBOL(g_pool_prof), sizeof(g_pool_prof));
+    (void)hipMemcpyFromSymbol(rois, HIP_SYMBOL(g_pool_prof_rois), sizeof(g_pool_prof_rois));
+    if (reset) {
+        static unsigned long long zt[kPoolProfSlots][4];
+        static unsigned zr[kPoolProfSlots];
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pool_prof), zt, sizeof(zt));
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_pool_prof_rois), zr, sizeof(zr));
+    }
+    return 0;
+}
+#endif
+
+namespace {
+struct FwdWs {
+    int* list;
+    int* cnt;
+    int* sched;  // wave kernel: RoIs handed out per (image, channel group) pair
+    size_t bytes;
+};
+FwdWs carve_fwd(void* ws, int64_t R, int N, int C) {
+    Carver c(ws);
+    FwdWs w{};
+    w.list = c.take<int>(static_cast<size_t>(N + 1) * R);
+    w.cnt = c.take<int>(N + 1);
+    w.sched = c.take<int>(static_cast<size_t>(N + 1) * (C / 4 + 1));
+    w.bytes = c.used();
+    return w;
+}
+
+// Launch plan of the wave-per-RoI forward: CG = 16 channel planes when they
+// fit the CU's LDS (one workgroup per CU), else 8 (two per CU when they fit),
+// else 4; wgs = the resident slots of the CUs the launch stream may use (at
+// most one workgroup per 8 RoIs of a pair).  The grid is persistent: every
+// workgroup pulls RoIs and takes over pairs until all are done.
+struct PxPlan {
+    int cg = 0, wgs = 0;
+    size_t lds = 0;
+};
+PxPlan px_plan(int64_t R, int C, int N, int H, int W, int PHW, hipStream_t st) {
+    PxPlan pl;
+    const size_t HW = static_cast<size_t>(H) * W;
+    if (N <= 0 || HW == 0 || PHW > 64 || H > 65535 || W > 65535) return pl;
+    constexpr size_t kReserve = 1024;  // static LDS + allocation rounding
+    const size_t HWs = (HW + 15) & ~static_cast<size_t>(15);
+    const size_t bnd = static_cast<size_t>(N + 1) * sizeof(int);
+    for (int cg : {16, 8, 4}) {
+        if (C % cg != 0) continue;
+        if (path_cfg().roi_cg && cg != path_cfg().roi_cg) continue;  // A/B override
+        const size_t tile = static_cast<size_t>(cg / 4) * HWs * sizeof(float4);
+        int per_cu = 0;
+        if (2 * (tile + bnd + kReserve) <= kLdsPerCu) per_cu = 2;
+        else if (tile + bnd + kReserve <= kLdsPerCu) per_cu = 1;
+        if (!per_cu) continue;
+        pl.cg = cg;
+        pl.lds = tile + bnd;
+        const int64_t pairs = static_cast<int64_t>(C / cg) * N;
+        int64_t per_pair = (R / N + 7) / 8;
+        per_pair = per_pair < 1 ? 1 : (per_pair > 64 ? 64 : per_pair);
+        int64_t wgs = static_cast<int64_t>(stream_cu_count(st)) * per_cu;
+        if (wgs > pairs * per_pair) wgs = pairs * per_pair;
+        if (path_cfg().roi_split > 0) wgs = pairs * path_cfg().roi_split;  // A/B override: workgroups per pair
+        pl.wgs = static_cast<int>(wgs < 1 ? 1 : (wgs > 65535 ? 65535 : wgs));
+        return pl;
+    }
+    return pl;
+}
+
+template <bool HEAD>
+int px_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
+              int PH, int PW, float ss, float* out, int32_t* argmax, int* sched, const HeadArgs& hd,
+              hipStream_t st) {
+    const int P = (N + 1) * (C / pl.cg);
+    if (hipMemsetAsync(sched, 0, sizeof(int) * static_cast<size_t>(P), st) != hipSuccess)
+        return check_launch("roi_pool_fwd_wave_kernel: scheduler reset");
+#define FRCNN_PX(CG)                                                                                     \
+    hipLaunchKernelGGL((roi_pool_fwd_wave_kernel<1024, CG, HEAD>), dim3(pl.wgs), dim3(1024), pl.lds, st, x, \
+                       rois, static_cast<int>(R), N, C, H, W, PH, PW, ss, out, argmax, sched, hd)
+    if (pl.cg == 16) FRCNN_PX(16);
+    else if (pl.cg == 8) FRCNN_PX(8);
+    else FRCNN_PX(4);
+#undef FRCNN_PX
+    FRCNN_LAUNCH_CHECK("roi_pool_fwd_wave_kernel");
+    return FRCNN_OK;
+}
+
+// Launch plan of the dense forward: CG = 16 channel planes when they fit the
+// CU's LDS with room for a RoI chunk, else 8, else 4 (two workgroups per CU
+// when two fit); cap = RoIs per geometry chunk from the LDS left over; split =
+// cost-balanced RoI shares per (image, channel group), sized so the grid fills
+// every resident slot once.
+struct DensePlan {
+    int cg = 0, cap = 0, split = 1;
+    size_t lds = 0;
+};
+DensePlan dense_plan(int C, int N, int H, int W, int PHW) {
+    DensePlan pl;
+    const size_t HW = static_cast<size_t>(H) * W;
+    if (N <= 0 || HW == 0 || PHW > 64 || H > 65535 || W > 65535) return pl;
+    const size_t HWs = (HW + 15) & ~static_cast<size_t>(15);
+    const size_t fixed = dense_fixed_bytes() + 64;  // + alignment slack
+    constexpr size_t kMinItems = 64;
+    for (int cg : {16, 8, 4}) {
+        if (C % cg != 0) continue;
+        if (path_cfg().roi_cg && cg != path_cfg().roi_cg) continue;  // A/B override
+        const size_t tile = static_cast<size_t>(cg / 4) * HWs * sizeof(float4);
+        const size_t need = tile + fixed + kMinItems * dense_item_bytes();
+        if (HWs * 16 * (cg / 4) >= (1u << 31) || need > kLdsPerCu) continue;
+        const int per_cu = 2 * need <= kLdsPerCu ? 2 : 1;
+        size_t cap = (kLdsPerCu / per_cu - tile - fixed) / dense_item_bytes();
+        cap = cap > 4096 ? 4096 : cap;
+        pl.cg = cg;
+        pl.cap = static_cast<int>(cap & ~static_cast<size_t>(15));
+        pl.lds = tile + fixed + static_cast<size_t>(pl.cap) * dense_item_bytes();
+        const int64_t wgs = static_cast<int64_t>(C / cg) * N;
+        const int64_t target = static_cast<int64_t>(device_cu_count()) * per_cu;
+        int64_t sp = (target + wgs - 1) / wgs;
+        if (path_cfg().roi_split > 0) sp = path_cfg().roi_split;  // A/B override
+        pl.split = static_cast<int>(sp < 1 ? 1 : (sp > 64 ? 64 : sp));
+        return pl;
+    }
+    return pl;
+}
+
+template <bool HEAD, bool LIST>
+int dense_launch(const DensePlan& pl, const float* x, const float* rois, const int* list, const int* cnt,
+                 int64_t R, int N, int C, int H, int W, int PH, int PW, float ss, float* out,
+                 int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
+    const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(pl.split),
+                    static_cast<unsigned>(LIST ? N : N + 1));
+    const bool fix7 = PH == 7 && PW == 7;
+#define FRCNN_DENSE(CG, FX)                                                                               \
+    hipLaunchKernelGGL((roi_pool_fwd_dense_kernel<1024, CG, FX, HEAD, LIST>), grid, dim3(1024), pl.lds, st, \
+                       x, rois, list, cnt, static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.cap,  \
+                       hd)
+    if (pl.cg == 16) {
+        if (fix7) FRCNN_DENSE(16, 7); else FRCNN_DENSE(16, 0);
+    } else if (pl.cg == 8) {
+        if (fix7) FRCNN_DENSE(8, 7); else FRCNN_DENSE(8, 0);
+    } else {
+        if (fix7) FRCNN_DENSE(4, 7); else FRCNN_DENSE(4, 0);
+    }
+#undef FRCNN_DENSE
+    FRCNN_LAUNCH_CHECK("roi_pool_fwd_dense_kernel");
+    return FRCNN_OK;
+}
+}  // namespace
+
+extern "C" size_t frcnn_roi_pool_fwd_workspace_size(int64_t R, int N, int C) {
+    if (R < 0 || N < 0 || C < 0) return 0;
+    return carve_fwd(nullptr, R, N, C).bytes;
+}
+
+extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, int N, int C,
+                                  int H, int W, int PH, int PW, float spatial_scale,
+                                  int rois_sorted, float* out, int32_t* argmax, void* workspace,
+                                  size_t ws_bytes, void* stream) {
+    FRCNN_REQUIRE(R >= 0 && N >= 0 && C >= 0 && H >= 0 && W >= 0, "frcnn_roi_pool_fwd: bad shape");
+    FRCNN_REQUIRE(PH > 0 && PW > 0 && PH * PW <= kMaxBins,
+                  "frcnn_roi_pool_fwd: output_size must have 1..%d bins", kMaxBins);
+    FRCNN_REQUIRE(R <= 0x7fffffff && N <= 65534, "frcnn_roi_pool_fwd: too many rois / images");
+    if (R == 0 || C == 0) return FRCNN_OK;
+    FRCNN_REQUIRE(x && rois && out && argmax, "frcnn_roi_pool_fwd: null pointer");
+    hipStream_t st = as_stream(stream);
+    const int path = path_cfg().roi_fwd;
+    const PxPlan xp = (rois_sorted && (path == kPathAuto || path == kPathWave))
+                          ? px_plan(R, C, N, H, W, PH * PW, st)
+                          : PxPlan{};
+    if (xp.cg) {
+        FwdWs w = carve_fwd(workspace, R, N, C);
+        FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_fwd: workspace %zu < %zu",
+                      ws_bytes, w.bytes);
+        return px_launch<false>(xp, x, rois, R, N, C, H, W, PH, PW, spatial_scale, out, argmax, w.sched,
+                                HeadArgs{}, st);
+    }
+    const DensePlan pl = path == kPathGeneric ? DensePlan{} : dense_plan(C, N, H, W, PH * PW);
+    if (pl.cg && rois_sorted)
+        return dense_launch<false, false>(pl, x, rois, nullptr, nullptr, R, N, C, H, W, PH, PW,
+                                          spatial_scale, out, argmax, HeadArgs{}, st);
+    if (pl.cg) {  // any RoI order: per-image lists first
+        FwdWs w = carve_fwd(workspace, R, N, C);
+        FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_fwd: workspace %zu < %zu",
+                      ws_bytes, w.bytes);
+        hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, rois, static_cast<int>(R), N,
+                           w.list, w.cnt);
+        FRCNN_LAUNCH_CHECK("roi_lists_kernel");
+        int rc = dense_launch<false, true>(pl, x, rois, w.list, w.cnt, R, N, C, H, W, PH, PW, spatial_scale,
+                                           out, argmax, HeadArgs{}, st);
+        if (rc) return rc;
+        hipLaunchKernelGGL(roi_pool_invalid_fill_kernel, dim3(64), dim3(256), 0, st, w.list, w.cnt,
+                           static_cast<int>(R), N, static_cast<size_t>(C) * PH * PW, out, argmax);
+        FRCNN_LAUNCH_CHECK("roi_pool_invalid_fill_kernel");
+        return FRCNN_OK;
+    }
+    // generic path: one workgroup per RoI, gathers from L1/L2
+    const size_t total = static_cast<size_t>(C) * PH * PW;
+    const bool aligned = (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
+                         (reinterpret_cast<uintptr_t>(argmax) % 16 == 0);
+    if (total % 4 == 0 && aligned)
+        hipLaunchKernelGGL(roi_pool_fwd_kernel<true>, dim3(static_cast<unsigned>(R)), dim3(256), 0,
+                           st, x, rois, N, C, H, W, PH, PW, spatial_scale, out, argmax);
+    else
+        hipLaunchKernelGGL(roi_pool_fwd_kernel<false>, dim3(static_cast<unsigned>(R)), dim3(256), 0,
+                           st, x, rois, N, C, H, W, PH, PW, spatial_scale, out, argmax);
+    FRCNN_LAUNCH_CHECK("roi_pool_fwd_kernel");
+    return FRCNN_OK;
+}
+
+extern "C" int frcnn_roi_pool_fwd_head(const float* x, const float* rois, const float* roi_inds,
+                                       int64_t R, int N, int C, int H, int W, int PH, int PW,
+                                       float img_h, float img_w, float spatial_scale,
+                                       int rois_sorted, float* boxes, float* out, int32_t* argmax,
+                                       void* workspace, size_t ws_bytes, void* stream) {
+    FRCNN_REQUIRE(R >= 0 && N >= 0 && C >= 0 && H >= 0 && W >= 0, "frcnn_roi_pool_fwd_head: bad shape");
+    FRCNN_REQUIRE(PH > 0 && PW > 0 && PH * PW <= kMaxBins,
+                  "frcnn_roi_pool_fwd_head: output_size must have 1..%d bins", kMaxBins);
+    FRCNN_REQUIRE(R <= 0x7fffffff && N <= 65534, "frcnn_roi_pool_fwd_head: too many rois / images");
+    if (R == 0) return FRCNN_OK;
+    FRCNN_REQUIRE(rois && roi_inds && boxes, "frcnn_roi_pool_fwd_head: null pointer");
+    const int path = path_cfg().roi_fwd;
+    const bool aligned = reinterpret_cast<uintptr_t>(rois) % 16 == 0;
+    const PxPlan xp = (rois_sorted && C > 0 && aligned && (path == kPathAuto || path == kPathWave))
+                          ? px_plan(R, C, N, H, W, PH * PW, as_stream(stream))
+                          : PxPlan{};
+    if (xp.cg) {  // transform + pack inside the pool kernel
+        FRCNN_REQUIRE(x && out && argmax, "frcnn_roi_pool_fwd_head: null pointer");
+        FwdWs w = carve_fwd(workspace, R, N, C);
+        FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_fwd_head: workspace %zu < %zu",
+                      ws_bytes, w.bytes);
+        const HeadArgs hd{roi_inds, img_h, img_w, static_cast<float>(H), static_cast<float>(W), boxes};
+        return px_launch<true>(xp, x, rois, R, N, C, H, W, PH, PW, spatial_scale, out, argmax, w.sched, hd,
+                               as_stream(stream));
+    }
+    const DensePlan pl = (rois_sorted && C > 0 && path != kPathGeneric)
+                             ? dense_plan(C, N, H, W, PH * PW)
+                             : DensePlan{};
+    if (!pl.cg || reinterpret_cast<uintptr_t>(rois) % 16 != 0) {
+        int rc = frcnn_roi_transform(rois, roi_inds, R, img_h, img_w, H, W, boxes, stream);
+        if (rc != FRCNN_OK) return rc;
+        if (C == 0) return FRCNN_OK;
+        return frcnn_roi_pool_fwd(x, boxes, R, N, C, H, W, PH, PW, spatial_scale, rois_sorted, out,
+                                  argmax, workspace, ws_bytes, stream);
+    }
+    FRCNN_REQUIRE(x && out && argmax, "frcnn_roi_pool_fwd_head: null pointer");
+    const HeadArgs hd{roi_inds, img_h, img_w, static_cast<float>(H), static_cast<float>(W), boxes};
+    return dense_launch<true, false>(pl, x, rois, nullptr, nullptr, R, N, C, H, W, PH, PW, spatial_scale,
+                                     out, argmax, hd, as_stream(stream));
+}
+
+namespace {
+struct BwdWs {
+    uint64_t* cmask;
+    uint8_t* code;
+    int* list;
+    int* cnt;
+    size_t bytes;
+};
+BwdWs carve_bwd(void* ws, int64_t R, int N, int PH, int PW) {
+    Carver c(ws);
+    BwdWs w{};
+    w.cmask = c.take<uint64_t>(static_cast<size_t>(R) * PH * PW);
+    w.code = c.take<uint8_t>(static_cast<size_t>(R) * PH * PW);
+    w.list = c.take<int>(static_cast<size_t>(N + 1) * R);
+    w.cnt = c.take<int>(N + 1);
+    w.bytes = c.used();
+    return w;
+}
+constexpr size_t kPlaneBudget = 64 * 1024;       // LDS per workgroup for planes (plain kernel)
+constexpr int kBwdRing = 8;                      // RoIs in flight per wave (ring kernel)
+constexpr size_t kPlaneBudgetRing = 144 * 1024;  // ring kernel: one workgroup per CU
+}  // namespace
+
+extern "C" size_t frcnn_roi_pool_bwd_workspace_size(int64_t R, int N, int PH, int PW) {
+    if (R < 0 || N < 0 || PH <= 0 || PW <= 0) return 0;
+    return carve_bwd(nullptr, R, N, PH, PW).bytes;
+}
+
+extern "C" int frcnn_roi_pool_bwd(const float* grad, const float* rois, const int32_t* argmax,
+                                  int64_t R, int N, int C, int H, int W, int PH, int PW,
+                                  float spatial_scale, float* grad_in, void* workspace,
+                                  size_t ws_bytes, void* stream) {
+    FRCNN_REQUIRE(R >= 0 && N >= 0 && C >= 0 && H >= 0 && W >= 0, "frcnn_roi_pool_bwd: bad shape");
+    FRCNN_REQUIRE(PH > 0 && PW > 0 && PH * PW <= kMaxBins, "frcnn_roi_pool_bwd: bad output_size");
+    FRCNN_REQUIRE(R <= 0x7fffffff, "frcnn_roi_pool_bwd: too many rois");
+    hipStream_t st = as_stream(stream);
+    const size_t HW = static_cast<size_t>(H) * W;
+    if (N == 0 || C == 0 || HW == 0) return FRCNN_OK;
+    FRCNN_REQUIRE(grad_in, "frcnn_roi_pool_bwd: null grad_in");
+    if (R == 0) {
+        if (hipMemsetAsync(grad_in, 0, sizeof(float) * N * C * HW, st) != hipSuccess)
+            return check_launch("frcnn_roi_pool_bwd memset");
+        return FRCNN_OK;
+    }
+    FRCNN_REQUIRE(grad && rois && argmax, "frcnn_roi_pool_bwd: null pointer");
+    BwdWs w = carve_bwd(workspace, R, N, PH, PW);
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_bwd: workspace %zu < %zu",
+                  ws_bytes, w.bytes);
+    FRCNN_REQUIRE(N <= 65535, "frcnn_roi_pool_bwd: N > 65535");
+    hipLaunchKernelGGL(roi_bwd_prep_kernel, dim3(static_cast<unsigned>(R)), dim3(256), 0, st, rois,
+                       H, W, PH, PW, spatial_scale, w.cmask, w.code);
+    FRCNN_LAUNCH_CHECK("roi_bwd_prep_kernel");
+    hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, rois, static_cast<int>(R),
+                       N, w.list, w.cnt);
+    FRCNN_LAUNCH_CHECK("roi_lists_kernel");
+    const size_t plane_bytes = HW * sizeof(float);
+    const int PHW = PH * PW;
+    const bool ring = PHW <= 64 && path_cfg().roi_bwd != kPathPlain;
+    if (ring && plane_bytes <= kPlaneBudgetRing) {
+        // Every wave owns one (image, channel) plane and walks all of the
+        // image's RoIs, so the work per wave is fixed: spread the N*C waves
+        // evenly, one workgroup per CU (ceil(N*C / CUs) waves each) where the
+        // LDS allows -- a 2:1 mix of busy and half-idle CUs cost 1.35x.
+        const int64_t waves = static_cast<int64_t>(N) * C;
+        int64_t cpw = (waves + device_cu_count() - 1) / device_cu_count();
+        const int64_t lds_cap = static_cast<int64_t>(kPlaneBudgetRing / plane_bytes);
+        cpw = cpw > 16 ? 16 : cpw;
+        cpw = cpw > lds_cap ? lds_cap : cpw;
+        cpw = cpw > C ? C : cpw;
+        cpw = cpw < 1 ? 1 : cpw;
+        const int icpw = static_cast<int>(cpw);
+        dim3 grid((C + icpw - 1) / icpw, N);
+        hipLaunchKernelGGL(roi_pool_bwd_pf_kernel<kBwdRing>, grid, dim3(64 * icpw), icpw * plane_bytes, st,
+                           grad, argmax, w.cmask, w.code, w.list, w.cnt, static_cast<int>(R), C,
+                           static_cast<int>(HW), PHW, PW, icpw, grad_in);
+    } else if (plane_bytes <= kPlaneBudget) {
+        int cpw = static_cast<int>(kPlaneBudget / plane_bytes);
+        cpw = cpw > 16 ? 16 : cpw;
+        cpw = cpw > C ? C : cpw;
+        dim3 grid((C + cpw - 1) / cpw, N);
+        hipLaunchKernelGGL(roi_pool_bwd_kernel<true>, grid, dim3(64 * cpw), cpw * plane_bytes, st,
+                           grad, argmax, w.cmask, w.list, w.cnt, static_cast<int>(R), C,
+                           static_cast<int>(HW), PHW, cpw, grad_in);
+    } else {
+        const int cpw = 4;
+        dim3 grid((C + cpw - 1) / cpw, N);
+        hipLaunchKernelGGL(roi_pool_bwd_kernel<false>, grid, dim3(64 * cpw), 0, st, grad, argmax,
+                           w.cmask, w.list, w.cnt, static_cast<int>(R), C, static_cast<int>(HW),
+                           PHW, cpw, grad_in);
+    }
+    FRCNN_LAUNCH_CHECK("roi_pool_bwd_kernel");
+    return FRCNN_OK;
+}
