@@ -68,7 +68,15 @@ def main():
             "stage": us(tl[:, 2] - tl[:, 1]), "compute": us(tl[:, 3] - tl[:, 2]),
             "end": us(tl[:, 3] - t0),
         }
+        # per workgroup: pooling time by XCD (dispatch order round-robins the
+        # workgroup id over the 8 XCDs) and by image (slowest grid dimension)
+        comp = (t[:, 3] - t[:, 2]) / 100.0
+        G = x.size(1) // (16 if x.size(2) * x.size(3) <= 2400 else 8)
+        split = max(1, len(used) // max(1, (N + 1) * G))
+        by_xcd = [round(float(np.mean(comp[live & (used % 8 == k)])), 2) for k in range(8)]
+        by_img = [round(float(np.mean(comp[live & (used // (G * split) == b)])), 2) for b in range(N)]
         res.append({
+            "compute_by_xcd": by_xcd, "compute_by_image": by_img,
             "events_us": e0.elapsed_time(e1) * 1e3, "span_us": us(t[:, 3].max() - t0),
             "wgs": int(len(used)), "live_wgs": int(live.sum()),
             "rois_per_wg": [int(nro[used][live].min()), float(nro[used][live].mean()), int(nro[used][live].max())],
