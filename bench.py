@@ -84,6 +84,9 @@ def parse():
     ap.add_argument("--roi-split", default="auto",
                     help="RoI shares per (image, channel group) of the RoIPool forward "
                          "(frcnn_set_path roi_pool_split): auto | 1 | 2 | ...")
+    ap.add_argument("--input-sets", type=int, default=0,
+                    help="distinct input sets the steps cycle through (0 = enough for > 320 MiB, "
+                         "i.e. more than the Infinity Cache; 1 = the same inputs every step)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-baseline sample (rank 0, N=1 only); 0 disables")
     ap.add_argument("--cpu-images", type=int, default=10, help="minimum timed CPU images (median)")
@@ -138,16 +141,32 @@ def resolve_config(args, world):
     return "cfg2" if world == 1 else "cfg3"
 
 
-def make_inputs(cfg, images, device):
+def make_inputs(cfg, images, device, seed=0):
     from replication_faster_rcnn_amd import synth
     c = synth.CONFIGS[cfg]
     K = 3 * len(c["scales"])
     A = c["feat_h"] * c["feat_w"] * K
-    sc = torch.from_numpy(np.stack([synth.rpn_scores(A, 0, i) for i in images])).to(device)
-    de = torch.from_numpy(np.stack([synth.rpn_deltas(A, 0, i) for i in images])).to(device)
-    x = torch.from_numpy(np.stack([synth.features(c["C"], c["feat_h"], c["feat_w"], 0, i)
+    sc = torch.from_numpy(np.stack([synth.rpn_scores(A, seed, i) for i in images])).to(device)
+    de = torch.from_numpy(np.stack([synth.rpn_deltas(A, seed, i) for i in images])).to(device)
+    x = torch.from_numpy(np.stack([synth.features(c["C"], c["feat_h"], c["feat_w"], seed, i)
                                    for i in images])).to(device)
     return c, sc, de, x
+
+
+INPUT_SPAN = 320 << 20  # bytes of distinct inputs the timed steps cycle through (> 256 MiB MALL)
+
+
+def make_input_sets(cfg, images, device, n_sets):
+    """Input sets the steps cycle through (set s seeded by s, image by its global
+    index): with more distinct bytes than the 256 MiB Infinity Cache, every
+    step reads its scores / deltas / features from HBM, not from a cache the
+    previous identical step left warm."""
+    c, sc, de, x = make_inputs(cfg, images, device, 0)
+    per = sum(t.numel() * t.element_size() for t in (sc, de, x))
+    if n_sets <= 0:
+        n_sets = int(min(64, max(2, -(-INPUT_SPAN // per))))
+    sets = [(sc, de, x)] + [make_inputs(cfg, images, device, s)[1:] for s in range(1, n_sets)]
+    return c, sets, per
 
 
 # ------------------------------------------------------------- CPU baseline
@@ -336,13 +355,14 @@ def gather(rois, idx, cnt, n_total, backend):
     return tuple(t.to(rois.device, non_blocking=True) for t in out)
 
 
-def inference_step_fn(args, c, sc, de, x, base, world, n_total, backend, ev):
+def inference_step_fn(args, c, sets, base, world, n_total, backend, ev):
     """cfg1-4: propose -> (all-gather of detections) -> RoI transform + pack +
     RoIPool forward (nets/rpn.py:102-138, nets/heads.py:42-48).  Every buffer
     and event is allocated once, outside the timed steps: proposal outputs per
     proposal stream (reused once the pool that read them has finished), one set
     of pooled outputs on the pool stream."""
     from replication_faster_rcnn_amd import ops
+    sc, de, x = sets[0]
     N, dev = sc.size(0), sc.device
     post = c["post_nms"]
     C = x.size(1)
@@ -372,6 +392,7 @@ def inference_step_fn(args, c, sc, de, x, base, world, n_total, backend, ev):
     def step(timed):
         j = k_step[0] % nps
         s_prop = s_props[j]
+        sc, de, x = sets[k_step[0] % len(sets)]
         k_step[0] += 1
         rois, idx, cnt = prop_out[j]
         with on_prop[j]:
@@ -411,7 +432,7 @@ def inference_step_fn(args, c, sc, de, x, base, world, n_total, backend, ev):
     return step
 
 
-def train_step_fn(args, c, sc, de, x, base, first_image, ev):
+def train_step_fn(args, c, sets, base, first_image, ev):
     """cfg5 (training step, train.py:59-127 minus the dense layers): propose
     (12000->600) -> anchor targets of every image -> proposal targets of every
     image (numpy's MT19937 stream kept on the device, sync-free, in the
@@ -429,6 +450,7 @@ def train_step_fn(args, c, sc, de, x, base, first_image, ev):
     RoIPool forward + backward of step k on a third, beside AT(k+1)."""
     from replication_faster_rcnn_amd import anchors as A, ops, synth, targets
     from replication_faster_rcnn_amd.utils import rng_state_to_device
+    sc, de, x = sets[0]
     N, dev = sc.size(0), sc.device
     S = 128
     anchors = A.generate_anchors(base, 16, c["feat_w"], c["feat_h"]).to(dev)
@@ -461,6 +483,7 @@ def train_step_fn(args, c, sc, de, x, base, first_image, ev):
 
     def step(timed):
         j = k_step[0] % 2
+        sc, de, x = sets[k_step[0] % len(sets)]
         k_step[0] += 1
         with torch.cuda.stream(s_prep):
             if sample_done[j] is not None:
@@ -534,16 +557,16 @@ def main():
     mine = fdist.shard(n_total, rank, world)
     if len(mine) == 0:
         raise SystemExit(f"rank {rank}: no images ({n_total} over {world} ranks)")
-    c, sc, de, x = make_inputs(cfg, mine, dev)
-    N = sc.size(0)
+    c, sets, set_bytes = make_input_sets(cfg, mine, dev, args.input_sets)
+    N = sets[0][0].size(0)
     base = A.generate_anchor_base_device(anchor_scales=c["scales"])
     ev = {"fwd": [], "bwd": [], "i": 0,  # timing events allocated before the timed steps
           "pairs": [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                     for _ in range(args.steps)]}
     if train:
-        step = train_step_fn(args, c, sc, de, x, base, mine.start, ev)
+        step = train_step_fn(args, c, sets, base, mine.start, ev)
     else:
-        step = inference_step_fn(args, c, sc, de, x, base, world, n_total, backend, ev)
+        step = inference_step_fn(args, c, sets, base, world, n_total, backend, ev)
 
     for _ in range(args.warmup):
         cnt = step(False)
@@ -571,7 +594,7 @@ def main():
     if world > 1 and not train:
         g_rois, g_idx, g_cnt = step.gathered["last"]
         gathered = {"images": int(g_cnt.numel()), "rois": int(g_cnt.sum().item())}
-    C, H, W = x.shape[1:]
+    C, H, W = sets[0][2].shape[1:]
     alg_bytes = N * C * H * W * 4 + R * 20 + 2 * R * C * 49 * 4
     fwd_ms = float(np.mean([a.elapsed_time(b) for a, b in ev["fwd"]]))
     # the dominant kernel: RoIPool fwd (inference), RoIPool bwd (training step;
@@ -599,7 +622,10 @@ def main():
         "metric": "images/sec through RPN proposal+NMS+RoIPool; RoIPool HBM GB/s vs peak",
         "value": images / el, "unit": "images/sec", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
-        "scaling": scaling, "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+        "scaling": scaling, "vs_baseline": None, "dtype": "fp32",
+        "data": f"synthetic, {len(sets)} input sets of {set_bytes / 2**20:.1f} MiB cycled (HBM-resident, "
+                f"{len(sets) * set_bytes / 2**20:.0f} MiB > the 256 MiB Infinity Cache)"
+                if len(sets) * set_bytes > (256 << 20) else f"synthetic, {len(sets)} input set(s) cycled",
         "config": {"workload": workload, "global_batch": n_total,
                    "parallelism": f"dp{world} (per-image sharding)", "streams": args.streams,
                    "prop_streams": args.prop_streams if (args.streams == 2 and not train) else 1,

@@ -681,6 +681,28 @@ __device__ int chunk_sweep(const uint64_t* __restrict__ colT, int cc, int post, 
     return kcount;
 }
 
+// Phase probe of the fused kernel (instrumented builds only, -DFRCNN_PROP_PROF,
+// tools/probe_propose.py): realtime clock (100 MHz) per (image, mode) at entry,
+// keys loaded, first select done, chunk compacted, chunk sorted, exit.
+#ifdef FRCNN_PROP_PROF
+__device__ unsigned long long g_prop_prof[3][256][8];
+#define PRPROF(k)                                                                            \
+    do {                                                                                     \
+        if (threadIdx.x == 0 && blockIdx.x < 256)                                            \
+            g_prop_prof[MODE][blockIdx.x][k] = __builtin_amdgcn_s_memrealtime();             \
+    } while (0)
+extern "C" int frcnn_debug_prop_prof(unsigned long long* out, int reset) {
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prop_prof), sizeof(g_prop_prof));
+    if (reset) {
+        static unsigned long long z[3][256][8];
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_prop_prof), z, sizeof(z));
+    }
+    return 0;
+}
+#else
+#define PRPROF(k) do {} while (0)
+#endif
+
 // MODE 0: the lazy path, every chunk; MODE 1 / 2: the hybrid path's two
 // per-image halves (see above).
 template <int KPT, int MODE>
@@ -699,6 +721,7 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
 
     const int n = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    PRPROF(0);
     const uint64_t* keys = keys_all + static_cast<size_t>(n) * A;
     const float4* boxes = boxes_all + static_cast<size_t>(n) * A;
     float4* orois = out_rois + static_cast<size_t>(n) * post;
@@ -749,9 +772,11 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
         }
         __syncthreads();
     }
+    PRPROF(1);
     while (r_done < P && kcount < post) {
         const int r_end = min(r_done + kChunk, P);
         const uint64_t T = select_rank<KPT>(sk, A, static_cast<unsigned>(r_end), hist, sh);
+        if (r_done == 0) PRPROF(2);
         if (tid == 0) sh.ccount = 0;
         __syncthreads();
 #pragma unroll
@@ -764,6 +789,7 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
         }
         __syncthreads();
         const int cc = r_end - r_done;  // == sh.ccount (keys are unique)
+        if (r_done == 0) PRPROF(3);
         // ---- sort of the chunk, ascending: every wave bitonic-sorts its 64 keys
         // with shuffles; a key's final position is its rank = the number of keys
         // below it over the 16 sorted runs (binary searches; valid keys are
@@ -805,7 +831,9 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
             carea[tid] = box_area(b);
         }
         __syncthreads();
+        if (r_done == 0) PRPROF(4);
         if (MODE == 1) {  // hand the sorted first chunk to chunk_colmask_kernel
+            PRPROF(5);
             if (tid < cc) {
                 hw.cbox[static_cast<size_t>(n) * kChunk + tid] = cbox[tid];
                 hw.ckey[static_cast<size_t>(n) * kChunk + tid] = key;
@@ -892,6 +920,7 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
         oidx[s] = -1;
     }
     if (tid == 0) out_count[n] = kcount;
+    PRPROF(5);
 }
 
 static size_t fused_lds_bytes(int post) {

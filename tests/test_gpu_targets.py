@@ -256,3 +256,49 @@ def test_anchor_targets_prepare_sample_split(rng_guard):
         assert torch.equal(l0, l1)
         assert torch.equal(r0, r1)
     assert torch.equal(rng_a, rng_b)
+
+
+def test_cfg5_full_batch_targets(rng_guard):
+    """BASELINE configs[4] at full batch: 16 images of 600x600 (38x38x9 anchors,
+    32 gt slots with 1..32 valid), HIP proposals (12000 -> 600), then ONE batched
+    AnchorTargetCreator call and ONE batched ProposalTargetCreator call on the
+    global numpy RNG -- vs the reference's per-image loops (train.py:71,91: all
+    anchor targets, then all proposal targets), RNG state compared after each."""
+    from replication_faster_rcnn_amd import anchors as A, ops
+    c = synth.CONFIGS["cfg5"]
+    N, G, img = c["batch"], 32, c["img_h"]
+    anchors = orc.generate_anchors(orc.generate_anchor_base(), 16, c["feat_w"], c["feat_h"])
+    nA = len(anchors)
+    bl = [synth.gt_boxes(img, img, G, 5, i, n_valid=1 + (7 * i) % 32) for i in range(N)]
+    boxes = np.stack([b for b, _ in bl])
+    labels = np.stack([l for _, l in bl])
+    sc = np.stack([synth.rpn_scores(nA, 5, i) for i in range(N)])
+    de = np.stack([synth.rpn_deltas(nA, 5, i) for i in range(N)])
+    dev = torch.device("cuda", 0)
+    rois, _, cnt = ops.propose(torch.from_numpy(sc).to(dev), torch.from_numpy(de).to(dev), img_w=img,
+                               img_h=img, pre_nms=c["pre_nms"], post_nms=c["post_nms"],
+                               anchor_base=A.generate_anchor_base_device(), feat_h=c["feat_h"],
+                               feat_w=c["feat_w"])
+    np.random.seed(2024)
+    reg, lab = targets.anchor_targets(boxes, labels, anchors)
+    s_roi, s_reg, s_lab, s_cnt = targets.proposal_targets(rois, cnt, boxes, labels)
+    st_dev = np.random.get_state()
+    np.random.seed(2024)
+    for i in range(N):
+        v = labels[i] != -1
+        oreg, olab = orc.anchor_target(boxes[i, v], anchors)
+        assert np.array_equal(lab[i].cpu().numpy(), olab), f"anchor labels, image {i}"
+        np.testing.assert_allclose(reg[i].cpu().numpy(), oreg, rtol=1e-12, atol=0)
+    rc = rois.cpu().numpy()
+    for i in range(N):
+        v = labels[i] != -1
+        k0 = int(cnt[i])
+        o_roi, o_reg, o_lab = orc.proposal_target(rc[i, :k0], boxes[i, v], labels[i][v])
+        k = int(s_cnt[i])
+        assert k == len(o_roi), f"image {i}"
+        assert np.array_equal(s_roi[i, :k].cpu().numpy(), o_roi), f"sampled rois, image {i}"
+        assert np.array_equal(s_lab[i, :k].cpu().numpy(), o_lab), f"sampled labels, image {i}"
+        np.testing.assert_allclose(s_reg[i, :k].cpu().numpy(), o_reg, rtol=1e-12, atol=1e-15)
+    st_ref = np.random.get_state()
+    assert st_dev[2] == st_ref[2]
+    assert np.array_equal(st_dev[1], st_ref[1])
