@@ -581,10 +581,13 @@ __device__ __forceinline__ const float4* tile_px(const float4* q4, int p) {
 // after every real one instead of holding CUs between them.
 // (Measured alternatives -- RoI bins packed 64 per wave, bins sorted by window
 // shape per image or per RoI block -- are slower: DESIGN.md §3.)
-template <int NT, int CG, bool HEAD>
+// FIX = PH = PW known at compile time (the 7x7 head): the 2 x CG output
+// stores of a RoI take immediate offsets from one base address.
+template <int NT, int CG, int FIX, bool HEAD>
 __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
-    const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W, int PH, int PW,
+    const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W, int PH_, int PW_,
     float ss, float* __restrict__ out, int32_t* __restrict__ argmax, int geo_cap, HeadArgs hd) {
+    const int PH = FIX ? FIX : PH_, PW = FIX ? FIX : PW_;
     constexpr int NP = CG / 4;
     extern __shared__ __attribute__((aligned(16))) float4 q4[];  // plane k at q4 + k * HWs; geometry after
     __shared__ int s_red[2 * (NT / 64)];
@@ -715,10 +718,12 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
             }
             if (act) {
                 const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
+                float* op = out + o;
+                int32_t* ap = argmax + o;
 #pragma unroll
                 for (int c = 0; c < CG; ++c) {
-                    out[o + static_cast<size_t>(c) * PHW] = mv[c];
-                    argmax[o + static_cast<size_t>(c) * PHW] = mi[c];
+                    op[c * PHW] = mv[c];
+                    ap[c * PHW] = mi[c];
                 }
             }
             k = __builtin_amdgcn_readfirstlane(kn);
@@ -1158,12 +1163,17 @@ template <bool HEAD>
 int px_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
               int PH, int PW, float ss, float* out, int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
     const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(pl.split), static_cast<unsigned>(N + 1));
-#define FRCNN_PX(CG)                                                                                    \
-    hipLaunchKernelGGL((roi_pool_fwd_wave_kernel<1024, CG, HEAD>), grid, dim3(1024), pl.lds, st, x, rois, \
+    const bool fix7 = PH == 7 && PW == 7;
+#define FRCNN_PX(CG, FX)                                                                                    \
+    hipLaunchKernelGGL((roi_pool_fwd_wave_kernel<1024, CG, FX, HEAD>), grid, dim3(1024), pl.lds, st, x, rois, \
                        static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd)
-    if (pl.cg == 16) FRCNN_PX(16);
-    else if (pl.cg == 8) FRCNN_PX(8);
-    else FRCNN_PX(4);
+    if (pl.cg == 16) {
+        if (fix7) FRCNN_PX(16, 7); else FRCNN_PX(16, 0);
+    } else if (pl.cg == 8) {
+        if (fix7) FRCNN_PX(8, 7); else FRCNN_PX(8, 0);
+    } else {
+        if (fix7) FRCNN_PX(4, 7); else FRCNN_PX(4, 0);
+    }
 #undef FRCNN_PX
     FRCNN_LAUNCH_CHECK("roi_pool_fwd_wave_kernel");
     return FRCNN_OK;
