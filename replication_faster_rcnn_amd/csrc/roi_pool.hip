@@ -596,7 +596,7 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
     const int c0 = blockIdx.x * CG;
     const int tid = threadIdx.x, lane = tid & 63;
     const int HW = H * W;
-    const int HWs = (HW + 15) & ~15;
+    const int HWs = (HW + 16) & ~15;  // + the zero sentinel pixel HW
     const int PHW = PH * PW;
     const int split = gridDim.y, z = blockIdx.y;
     const int N = gridDim.z - 1;
@@ -633,6 +633,7 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
     const int nmine = (nr - z + split - 1) / split;  // items z, z+split, ...
     PPROF_ROIS(nmine);
     const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+    if (tid < NP) const_cast<float4*>(tile_px<NP>(q4, HW))[16 * tid] = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int p = tid; p < HW; p += NT) {
         float v[CG];
 #pragma unroll
@@ -685,16 +686,32 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
             int4 g = geom_bin(gm, H, W, ph, pw);
             if (!act) g = make_int4(0, 0, 0, 0);
             const bool empty = g.y <= g.x || g.w <= g.z;
+            // the window's first pixel starts the scan (torchvision's strict '>'
+            // against -FLT_MAX, no per-channel initialisation); an empty window
+            // reads the zero sentinel pixel and keeps argmax -1
             float mv[CG];
             int mi[CG];
+            {
+                const int p0 = empty ? HW : g.x * W + g.z;
+                const float4* pp = tile_px<NP>(q4, p0);
+                float4 v[NP];
 #pragma unroll
-            for (int c = 0; c < CG; ++c) {
-                mv[c] = empty ? 0.0f : -FLT_MAX;
-                mi[c] = -1;
+                for (int q = 0; q < NP; ++q) v[q] = pp[16 * q];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int q = 0; q < NP; ++q) {
+                    const float vv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const bool gt = vv[j] > -FLT_MAX;
+                        mv[4 * q + j] = gt ? vv[j] : -FLT_MAX;
+                        mi[4 * q + j] = (gt && !empty) ? p0 : -1;
+                    }
+                }
             }
             for (int h = g.x; h < g.y; ++h) {
                 const int rb = h * W;
-                for (int w = g.z; w < g.w; ++w) {
+                for (int w = h == g.x ? g.z + 1 : g.z; w < g.w; ++w) {
                     const int ii = rb + w;
                     const float4* pp = tile_px<NP>(q4, ii);
                     float4 v[NP];
@@ -1137,7 +1154,7 @@ PxPlan px_plan(int C, int N, int H, int W, int PHW, hipStream_t st) {
     if (N <= 0 || HW == 0 || PHW > 64 || H > 65535 || W > 65535) return pl;
     constexpr size_t kReserve = 1024;  // static LDS + allocation rounding
     constexpr size_t kMinGeo = 64 * sizeof(int4);
-    const size_t HWs = (HW + 15) & ~static_cast<size_t>(15);
+    const size_t HWs = (HW + 16) & ~static_cast<size_t>(15);  // + the zero sentinel pixel
     for (int cg : {16, 8, 4}) {
         if (C % cg != 0) continue;
         if (path_cfg().roi_cg && cg != path_cfg().roi_cg) continue;  // A/B override
