@@ -62,6 +62,11 @@ def parse():
     ap.add_argument("--prop-streams", type=int, default=2,
                     help="with --streams 2 (inference configs): proposal layers of consecutive "
                          "steps round-robin over this many HIP streams")
+    ap.add_argument("--pool-on", default="prop", choices=("prop", "own"),
+                    help="with --streams 2 (inference): prop = each step's RoIPool runs on that step's "
+                         "proposal stream right after its proposals (consecutive steps on different "
+                         "streams overlap; no cross-stream waits), own = the RoIPool on a stream of "
+                         "its own, fed by events")
     ap.add_argument("--prop-cus", type=int, default=0,
                     help="with --streams 2: CUs reserved for the proposal streams (spread over the "
                          "XCDs); the RoIPool stream gets the rest.  0 = no reservation")
@@ -375,9 +380,12 @@ def inference_step_fn(args, c, sets, base, world, n_total, backend, ev):
     prop_out = [(torch.empty((N, post, 4), dtype=torch.float32, device=dev),
                  torch.empty((N, post), dtype=torch.int32, device=dev),
                  torch.empty((N,), dtype=torch.int32, device=dev)) for _ in range(nps)]
-    pool_out = (torch.empty((N * post, C, 7, 7), dtype=torch.float32, device=dev),
-                torch.empty((N * post, C, 7, 7), dtype=torch.int32, device=dev),
-                torch.empty((N * post, 5), dtype=torch.float32, device=dev))
+    pool_on_prop = args.pool_on == "prop" and args.streams == 2 and not args.host_io and args.prop_cus == 0
+    pool_outs = [(torch.empty((N * post, C, 7, 7), dtype=torch.float32, device=dev),
+                  torch.empty((N * post, C, 7, 7), dtype=torch.int32, device=dev),
+                  torch.empty((N * post, 5), dtype=torch.float32, device=dev))
+                 for _ in range(nps if pool_on_prop else 1)]
+    pool_out = pool_outs[0]
     ready = [torch.cuda.Event() for _ in range(nps)]
     done = [None] * nps          # the pool that last read prop_out[j]
     done_ev = [torch.cuda.Event() for _ in range(nps)]
@@ -395,6 +403,23 @@ def inference_step_fn(args, c, sets, base, world, n_total, backend, ev):
         sc, de, x = sets[k_step[0] % len(sets)]
         k_step[0] += 1
         rois, idx, cnt = prop_out[j]
+        if pool_on_prop:  # the step's proposals and RoIPool back to back on its stream
+            with on_prop[j]:
+                ops.propose(sc, de, img_w=c["img_w"], img_h=c["img_h"], pre_nms=c["pre_nms"],
+                            post_nms=post, anchor_base=base, feat_h=c["feat_h"], feat_w=c["feat_w"],
+                            out=prop_out[j])
+                if world > 1:  # the only collective: detections of all ranks
+                    gathered["last"] = gather(rois, idx, cnt, n_total, backend)
+                if timed:
+                    e0, e1 = ev["pairs"][ev["i"]]
+                    ev["i"] += 1
+                    e0.record(s_prop)
+                ops.roi_pool_head(x, rois.view(-1, 4), inds, 7, c["img_h"], c["img_w"],
+                                  rois_sorted=True, out=pool_outs[j])
+                if timed:
+                    e1.record(s_prop)
+                    ev["fwd"].append((e0, e1))
+            return cnt
         with on_prop[j]:
             if done[j] is not None:
                 s_prop.wait_event(done[j])  # the pool that read prop_out[j] (and d_in[j]) last time
@@ -629,6 +654,7 @@ def main():
         "config": {"workload": workload, "global_batch": n_total,
                    "parallelism": f"dp{world} (per-image sharding)", "streams": args.streams,
                    "prop_streams": args.prop_streams if (args.streams == 2 and not train) else 1,
+                   "pool_on": args.pool_on if (args.streams == 2 and not train) else None,
                    "host_io": bool(args.host_io), "roi_cg": args.roi_cg, "roi_split": args.roi_split,
                    "prop_cus": args.prop_cus if (args.streams == 2 and not train) else 0,
                    "propose_path": args.propose_path,
