@@ -20,9 +20,11 @@ torch.distributed.run itself as a child process before anything touches the
 GPU and exits with its code.  Images are seeded by global index, so every
 rank's shard is the same data as in the 1-GPU run.
 
-The proposal layer of step k+1 runs on its own HIP stream beside step k's
-RoIPool (--streams 1 serialises them); consecutive steps' proposal layers
-alternate over --prop-streams streams.  Every step does all of its work.
+Each step's proposal layer and RoIPool run back to back on one HIP stream, and
+consecutive steps alternate over --prop-streams (3) streams, so step k+1's
+proposals run beside step k's RoIPool without cross-stream waits (--streams 1
+serialises everything; --pool-on own puts the RoIPool on a stream of its own).
+Every step does all of its work.
 
 Prints ONE JSON line (rank 0): the metric of BASELINE.json, "roofline" (the
 dominant kernel's algorithmic HBM bytes over its HIP-event time on its launch
@@ -52,14 +54,14 @@ if ROOT not in sys.path:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="auto",
                     help="auto (cfg2 at N=1, cfg3 at N>1) | cfg1 | cfg2 | cfg3 | cfg4 | cfg5")
     ap.add_argument("--streams", type=int, default=2, choices=(1, 2),
                     help="2: the proposal layer of step k+1 runs on its own HIP stream beside "
                          "step k's RoIPool (each step still does all of its work)")
-    ap.add_argument("--prop-streams", type=int, default=2,
+    ap.add_argument("--prop-streams", type=int, default=3,
                     help="with --streams 2 (inference configs): proposal layers of consecutive "
                          "steps round-robin over this many HIP streams")
     ap.add_argument("--pool-on", default="prop", choices=("prop", "own"),
@@ -454,6 +456,11 @@ def inference_step_fn(args, c, sets, base, world, n_total, backend, ev):
             done[j] = done_ev[j]
         return cnt
     step.gathered = gathered
+
+    def alone():  # the dominant kernel by itself (after the timed steps): the last proposals
+        ops.roi_pool_head(sets[0][2], prop_out[0][0].view(-1, 4), inds, 7, c["img_h"], c["img_w"],
+                          rois_sorted=True, out=pool_outs[0])
+    step.alone = alone
     return step
 
 
@@ -549,9 +556,13 @@ def train_step_fn(args, c, sets, base, first_image, ev):
                 e[2].record(s_pool)
                 ev["fwd"].append((e[0], e[1]))
                 ev["bwd"].append((e[1], e[2]))
-        state.update(s_cnt=s_cnt, lab=lab, gi=gi)
+        state.update(s_cnt=s_cnt, lab=lab, gi=gi, am=am, bx=bx, xshape=tuple(x.shape))
         return s_cnt
     step.state = state
+
+    def alone():  # the dominant kernel (RoIPool backward) by itself, on the last step's inputs
+        ops._roi_pool_bwd(grad, state["bx"], state["am"], state["xshape"], 1.0)
+    step.alone = alone
     return step
 
 
@@ -626,6 +637,18 @@ def main():
     # same algorithmic bytes: grad + argmax read, rois, grad_in written)
     dom_ms = float(np.mean([a.elapsed_time(b) for a, b in ev["bwd"]])) if train else fwd_ms
     achieved = alg_bytes / (dom_ms * 1e-3) / 1e9
+    # the same kernel with the chip to itself (after the timed region; extra
+    # information -- `frac` above is the in-bench figure, beside the other
+    # streams' work)
+    step.alone()
+    torch.cuda.synchronize()
+    a0, a1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a0.record()
+    for _ in range(20):
+        step.alone()
+    a1.record()
+    torch.cuda.synchronize()
+    alone_ms = a0.elapsed_time(a1) / 20
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "roi_pool_bwd_traffic.json" if train
                          else "roi_pool_fwd_traffic.json")
@@ -665,7 +688,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "roi_pool_bwd_pf_kernel" if train else "roi_pool_fwd_wave_kernel<head>",
-                     "kernel_us": dom_ms * 1e3, "alg_bytes_per_launch": alg_bytes},
+                     "kernel_us": dom_ms * 1e3, "alg_bytes_per_launch": alg_bytes,
+                     "kernel_us_alone": alone_ms * 1e3,
+                     "frac_alone": alg_bytes / (alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
         "cpu_baseline": None,
         "host_issue_us_per_step": t_issue / args.steps * 1e6,
     }
