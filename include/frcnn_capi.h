@@ -56,7 +56,7 @@ int frcnn_probe_hw_ids(uint32_t* out, int nblocks, int spin, void* stream);
  *   "roi_pool_fwd"   : "auto" | "wave" (image tile in LDS, one wave per RoI; RoIs grouped by
  *                      image) | "dense" (image tile, bins packed 64 per wave; any RoI order)
  *                      | "generic" (one workgroup per RoI)
- *   "roi_pool_bwd"   : "auto" | "ring" (latency-hidden plane owner) | "plain"
+ *   "roi_pool_bwd"   : "auto" (leader-gather plane owner for 7-wide outputs, else ring) | "ring" (latency-hidden plane owner) | "plain"
  *   "propose"        : "auto" | "hybrid" | "lazy" (fused per image) | "wide" (chip-wide bitmask)
  *   "roi_pool_split" : "auto" | "1".."64" (RoI shares per image and channel group)
  *   "roi_pool_cg"    : "auto" | "4" | "8" | "16" (channels per RoIPool forward workgroup)

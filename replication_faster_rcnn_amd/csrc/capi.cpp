@@ -61,8 +61,9 @@ extern "C" int frcnn_set_path(const char* op, const char* path) {
         g_path.roi_fwd = aut ? kPathAuto : is(path, "generic") ? kPathGeneric
                                        : is(path, "dense")     ? kPathDense
                                                                : kPathWave;
-    } else if (is(op, "roi_pool_bwd") && (aut || is(path, "ring") || is(path, "plain"))) {
-        g_path.roi_bwd = is(path, "plain") ? kPathPlain : kPathAuto;
+    } else if (is(op, "roi_pool_bwd") &&
+               (aut || is(path, "ring") || is(path, "plain"))) {
+        g_path.roi_bwd = aut ? kPathAuto : is(path, "plain") ? kPathPlain : kPathRing;
     } else if (is(op, "propose") &&
                (aut || is(path, "hybrid") || is(path, "lazy") || is(path, "wide"))) {
         g_path.propose = aut ? kPathAuto : is(path, "hybrid") ? kPathHybrid

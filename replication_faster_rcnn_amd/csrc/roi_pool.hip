@@ -1093,6 +1093,262 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_pf_kernel(
     }
 }
 
+
+// Phase timer of the leader backward (-DFRCNN_BWD_PROF, tools/probe_bwd.py):
+// per wave, shader-clock cycles spent taking / refilling the ring (incl. the
+// load waits), in the neighbour exchanges, and applying to the plane.
+#ifdef FRCNN_BWD_PROF
+constexpr int kBwdProfWaves = 8192;
+__device__ unsigned long long g_bwd_prof[kBwdProfWaves][4];
+#define BPROF_T() __builtin_amdgcn_s_memtime()
+#else
+#define BPROF_T() 0ull
+#endif
+constexpr int kBwdXRow = 80;  // leader kernel: exchange-row entries per wave (int2)
+
+// Leader-gather plane-owner backward (PH*PW < 64, PW = PWT), the default.
+// Bins that share an argmax pixel all contain it, so their windows overlap;
+// when a RoI's overlaps are only between grid neighbours (the prep kernel's
+// per-RoI flag clear) the bins of one pixel lie in a 2x2 block.  The first of
+// them in bin order (no earlier neighbour -- left, up-left, up, up-right --
+// with the same argmax) leads: it reads the pixel once, adds its own gradient
+// and then those of its later neighbours with the same argmax (right or
+// down-left, down, down-right: ascending bin order) and writes once.  Every
+// pixel so sees the CPU summation order n -> ph -> pw in one read-add-write
+// per RoI, with no rank rounds.  Non-contributing neighbours add -0.0
+// (x + -0.0 == x for every plane value: sums started at +0.0 are never -0.0);
+// non-leaders read and write a dummy word of their own past the plane.  The neighbours'
+// (argmax, grad) pairs come through a per-wave LDS exchange row (one
+// ds_write_b64, eight ds_read_b64 at immediate offsets, conflict free) -- a
+// third of the LDS cycles of twelve ds_bpermute.  RoIs flagged by the prep kernel (tiny
+// windows overlapping beyond the neighbours) rank their bins from the full
+// overlap mask and apply in rounds, as the ring kernel.  D RoIs per step: the
+// exchanges of the D RoIs are issued before their read-add-writes go to the
+// plane in RoI order.
+template <int D, int PWT>
+__global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
+    const float* __restrict__ grad, const int32_t* __restrict__ argmax,
+    const uint64_t* __restrict__ cmask, const uint8_t* __restrict__ code,
+    const int* __restrict__ list, const int* __restrict__ cnt,
+    int R, int C, int HW, int HWs, int PHW, int CPW, float* __restrict__ grad_in) {
+    extern __shared__ __attribute__((aligned(16))) float planes[];
+    constexpr int PW = PWT;
+    static_assert(64 + 2 * (PW + 1) <= kBwdXRow, "exchange row too short");
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = blockIdx.y;
+    const int c = blockIdx.x * CPW + wid;
+    if (c >= C) return;  // whole wave; no workgroup barrier below
+    float* gplane = grad_in + (static_cast<size_t>(b) * C + c) * HW;
+    // HWs >= HW + 64: word HW + lane is lane's dummy (a word per lane, so the
+    // non-leaders' writes do not serialise on one bank)
+    float* plane = planes + static_cast<size_t>(wid) * HWs;
+    // Two exchange rows per wave: entry PW + 1 + k holds lane k's pair, linear in the lane so
+    // that a wave's reads at any fixed lane offset are bank-conflict free; a
+    // neighbour across the grid edge is masked by the lane's has_* flags.
+    // (LDS byte addresses; xrow = this lane's entry minus PW + 1 entries, the
+    // up-left neighbour; xbase = lane 0's entry.)
+    typedef __attribute__((address_space(3))) float lds_float;
+    const uint32_t xbase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_float*)planes)) +
+                           static_cast<uint32_t>(CPW * HWs * 4 + wid * 2 * kBwdXRow * 8 + (PW + 1) * 8);
+    const uint32_t xrow = xbase + 8 * lane - 8 * (PW + 1);
+    for (int i = lane; i < HWs; i += 64) plane[i] = 0.0f;
+    const int nr = cnt[b];
+    const int pw_i = lane % PW;
+    const bool has_l = pw_i > 0, has_r = pw_i < PW - 1;
+    const bool has_u = lane >= PW, has_d = lane + PW < PHW;
+    const bool has_ul = has_u && has_l, has_ur = has_u && has_r;
+    const bool has_dl = has_d && has_l, has_dr = has_d && has_r;
+    if (nr > 0) {
+        const int* lst = list + static_cast<size_t>(b) * R;  // wave-uniform: scalar loads
+        const bool act = lane < PHW;
+        const uint32_t kl = act ? lane : 0;
+        // the host guarantees R*C*PHW*4 < 2^31: byte offsets fit the descriptors
+        const uint32_t gb = static_cast<uint32_t>(R) * C * PHW * 4;
+        const uint32_t mb = static_cast<uint32_t>(R) * PHW;
+        const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(grad), 0, gb, 0x00020000);
+        const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(argmax), 0, gb, 0x00020000);
+        const auto rs_m = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(cmask), 0, mb * 8, 0x00020000);
+        const auto rs_c = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(code), 0, mb, 0x00020000);
+        const uint32_t cpb = static_cast<uint32_t>(c) * PHW * 4;
+        const uint32_t rpb = static_cast<uint32_t>(C) * PHW * 4;
+        int am_r[D];
+        float g_r[D];
+        uint32_t cd_r[D], cl_r[D], ch_r[D];
+        // list entries past the image's RoIs (the workspace is padded) are
+        // garbage: their slots are dead (argmax -1) and the buffer loads are
+        // range-checked
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int n = lst[d];
+            const uint32_t so = static_cast<uint32_t>(n) * rpb + cpb;
+            const uint32_t sm = static_cast<uint32_t>(n) * PHW;
+            am_r[d] = __builtin_amdgcn_raw_buffer_load_b32(rs_a, kl * 4, so, 0);
+            g_r[d] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g, kl * 4, so, 0));
+            cd_r[d] = __builtin_amdgcn_raw_buffer_load_b8(rs_c, kl, sm, 0);
+            const auto m = __builtin_amdgcn_raw_buffer_load_b64(rs_m, kl * 8, sm * 8, 0);
+            cl_r[d] = m[0];
+            ch_r[d] = m[1];
+            asm volatile("" ::: "memory");
+        }
+        unsigned long long tp[3] = {0, 0, 0};
+        for (int t0 = 0; t0 < nr; t0 += D) {
+            const unsigned long long p0 = BPROF_T();
+            int nx[D];
+#pragma unroll
+            for (int d = 0; d < D; ++d) nx[d] = lst[t0 + D + d];
+            int am[D], addr[D];
+            float g[D], s1[D], s3[D], s4[D];
+            bool slow[D];
+            // take the slot's argmax / grad / flag, then refill it with RoI t + D
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                uint32_t cd;
+                asm volatile("v_mov_b32 %0, %1" : "=v"(am[d]) : "v"(am_r[d]));
+                asm volatile("v_mov_b32 %0, %1" : "=v"(g[d]) : "v"(g_r[d]));
+                asm volatile("v_mov_b32 %0, %1" : "=v"(cd) : "v"(cd_r[d]));
+                const bool live = t0 + d < nr;
+                slow[d] = live && (__builtin_amdgcn_readfirstlane(cd) & 16) != 0;  // bin 0's code: the RoI flag
+                am[d] = live ? am[d] : -1;
+                am[d] = act ? am[d] : -2;
+                const int n = nx[d];
+                const uint32_t so = static_cast<uint32_t>(n) * rpb + cpb;
+                am_r[d] = __builtin_amdgcn_raw_buffer_load_b32(rs_a, kl * 4, so, 0);
+                g_r[d] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g, kl * 4, so, 0));
+                cd_r[d] = __builtin_amdgcn_raw_buffer_load_b8(rs_c, kl, static_cast<uint32_t>(n) * PHW, 0);
+            }
+            const unsigned long long p1 = BPROF_T();
+            // neighbour exchanges, two slots per LDS round trip (each slot its
+            // own row; plane-independent; LDS runs a wave's accesses in order,
+            // so a row's next write follows its reads); flagged RoIs rank
+            // their bins from the overlap mask, then the mask slot is refilled
+            static_assert(D % 2 == 0, "slots are exchanged in pairs");
+            auto lo = [](uint64_t q) { return static_cast<int>(static_cast<uint32_t>(q)); };
+            auto hi = [](uint64_t q) { return __builtin_bit_cast(float, static_cast<uint32_t>(q >> 32)); };
+#pragma unroll
+            for (int d0 = 0; d0 < D; d0 += 2) {
+                // per slot: one ds_write_b64 of this lane's pair, eight
+                // ds_read_b64 of the neighbours' at immediate offsets; one wait
+                // for both.  In asm, since other lanes' words are invisible to
+                // the compiler's ordering.  (64-bit scalars, not int2 vectors,
+                // as operands: a vector output's high half was read as its low.)
+                uint64_t q[2][8];
+                const uint64_t m0 = static_cast<uint32_t>(am[d0]) |
+                                    (static_cast<uint64_t>(__builtin_bit_cast(uint32_t, g[d0])) << 32);
+                const uint64_t m1 = static_cast<uint32_t>(am[d0 + 1]) |
+                                    (static_cast<uint64_t>(__builtin_bit_cast(uint32_t, g[d0 + 1])) << 32);
+                asm volatile(
+                    "ds_write_b64 %16, %18 offset:%c20\n\t"
+                    "ds_write_b64 %17, %19 offset:%c20\n\t"
+                    "ds_read_b64 %0, %16 offset:%c21\n\t"
+                    "ds_read_b64 %1, %16 offset:%c22\n\t"
+                    "ds_read_b64 %2, %16\n\t"
+                    "ds_read_b64 %3, %16 offset:%c23\n\t"
+                    "ds_read_b64 %4, %16 offset:%c24\n\t"
+                    "ds_read_b64 %5, %16 offset:%c25\n\t"
+                    "ds_read_b64 %6, %16 offset:%c26\n\t"
+                    "ds_read_b64 %7, %16 offset:%c27\n\t"
+                    "ds_read_b64 %8, %17 offset:%c21\n\t"
+                    "ds_read_b64 %9, %17 offset:%c22\n\t"
+                    "ds_read_b64 %10, %17\n\t"
+                    "ds_read_b64 %11, %17 offset:%c23\n\t"
+                    "ds_read_b64 %12, %17 offset:%c24\n\t"
+                    "ds_read_b64 %13, %17 offset:%c25\n\t"
+                    "ds_read_b64 %14, %17 offset:%c26\n\t"
+                    "ds_read_b64 %15, %17 offset:%c27\n\t"
+                    "s_waitcnt lgkmcnt(0)"
+                    : "=&v"(q[0][0]), "=&v"(q[0][1]), "=&v"(q[0][2]), "=&v"(q[0][3]), "=&v"(q[0][4]),
+                      "=&v"(q[0][5]), "=&v"(q[0][6]), "=&v"(q[0][7]), "=&v"(q[1][0]), "=&v"(q[1][1]),
+                      "=&v"(q[1][2]), "=&v"(q[1][3]), "=&v"(q[1][4]), "=&v"(q[1][5]), "=&v"(q[1][6]),
+                      "=&v"(q[1][7])
+                    : "v"(xrow), "v"(xrow + kBwdXRow * 8), "v"(m0), "v"(m1), "i"(8 * (PW + 1)),
+                      "i"(8 * PW), "i"(8), "i"(16), "i"(8 * (PW + 2)), "i"(8 * (2 * PW)),
+                      "i"(8 * (2 * PW + 1)), "i"(8 * (2 * PW + 2))
+                    : "memory");
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const int d = d0 + e;
+                    const int a = am[d];
+                    // q[e]: left, up, up-left, up-right, right, down-left, down, down-right
+                    const bool fol = static_cast<int>(has_l & (lo(q[e][0]) == a)) | (has_u & (lo(q[e][1]) == a)) |
+                                     (has_ul & (lo(q[e][2]) == a)) | (has_ur & (lo(q[e][3]) == a));
+                    // right and down-left never both match (they do not overlap)
+                    s1[d] = (has_r & (lo(q[e][4]) == a))    ? hi(q[e][4])
+                            : (has_dl & (lo(q[e][5]) == a)) ? hi(q[e][5])
+                                                            : -0.0f;
+                    s3[d] = (has_d & (lo(q[e][6]) == a)) ? hi(q[e][6]) : -0.0f;
+                    s4[d] = (has_dr & (lo(q[e][7]) == a)) ? hi(q[e][7]) : -0.0f;
+                    addr[d] = (a >= 0 && !fol) ? a : HW + lane;
+                    if (slow[d]) {  // addr = the bin's rank among the same-pixel bins
+                        int depth = 0;
+                        uint64_t pend = a >= 0 ? ((static_cast<uint64_t>(ch_r[d]) << 32) | cl_r[d]) : 0ull;
+                        const uint32_t xb = xbase + e * kBwdXRow * 8;
+                        while (__ballot(pend != 0)) {
+                            const int p = pend ? __ffsll(static_cast<unsigned long long>(pend)) - 1 : lane;
+                            pend &= pend - 1;
+                            int ap;
+                            asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                                         : "=v"(ap) : "v"(xb + 8 * p) : "memory");
+                            if (p != lane && ap == a) ++depth;
+                        }
+                        addr[d] = depth;
+                    }
+                    const uint32_t sm = static_cast<uint32_t>(nx[d]) * PHW;
+                    const auto m = __builtin_amdgcn_raw_buffer_load_b64(rs_m, kl * 8, sm * 8, 0);
+                    cl_r[d] = m[0];
+                    ch_r[d] = m[1];
+                }
+            }
+            const unsigned long long p2 = BPROF_T();
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                if (!slow[d]) {
+                    float v = plane[addr[d]];
+                    v = v + g[d];
+                    v = v + s1[d];
+                    v = v + s3[d];
+                    v = v + s4[d];
+                    plane[addr[d]] = v;
+                } else {  // ranked rounds, as the ring kernel
+                    const int a = am[d];
+                    for (int r = 0;; ++r) {
+                        if (a >= 0 && addr[d] == r) plane[a] += g[d];
+                        asm volatile("" ::: "memory");
+                        if (__ballot(a >= 0 && addr[d] > r) == 0) break;
+                    }
+                }
+                asm volatile("" ::: "memory");
+            }
+#ifdef FRCNN_BWD_PROF
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+            const unsigned long long p3 = BPROF_T();
+            tp[0] += p1 - p0;
+            tp[1] += p2 - p1;
+            tp[2] += p3 - p2;
+        }
+#ifdef FRCNN_BWD_PROF
+        const int gw = (blockIdx.y * gridDim.x + blockIdx.x) * CPW + wid;
+        if (lane == 0 && gw < kBwdProfWaves) {
+            g_bwd_prof[gw][0] = tp[0];
+            g_bwd_prof[gw][1] = tp[1];
+            g_bwd_prof[gw][2] = tp[2];
+            g_bwd_prof[gw][3] = nr;
+        }
+#else
+        (void)tp;
+#endif
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if ((HW & 3) == 0) {
+        const float4* s4 = reinterpret_cast<const float4*>(plane);
+        float4* d4 = reinterpret_cast<float4*>(gplane);
+        for (int i = lane; i < HW / 4; i += 64) d4[i] = s4[i];
+    } else {
+        for (int i = lane; i < HW; i += 64) gplane[i] = plane[i];
+    }
+}
+
 }  // namespace frcnn
 
 using namespace frcnn;
@@ -1110,6 +1366,16 @@ extern "C" int frcnn_roi_transform(const float* rois, const float* roi_inds, int
     return FRCNN_OK;
 }
 
+#ifdef FRCNN_BWD_PROF
+extern "C" int frcnn_debug_bwd_prof(unsigned long long* out, int reset) {
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_prof), sizeof(g_bwd_prof));
+    if (reset) {
+        static unsigned long long z[kBwdProfWaves][4];
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bwd_prof), z, sizeof(z));
+    }
+    return 0;
+}
+#endif
 #ifdef FRCNN_POOL_PROF
 extern "C" int frcnn_debug_pool_prof(unsigned long long* times, unsigned* rois, int reset) {
     (void)hipMemcpyFromSymbol(times, HIP_SYMBOL(g_pool_prof), sizeof(g_pool_prof));
@@ -1133,7 +1399,8 @@ struct FwdWs {
 FwdWs carve_fwd(void* ws, int64_t R, int N) {
     Carver c(ws);
     FwdWs w{};
-    w.list = c.take<int>(static_cast<size_t>(N + 1) * R);
+    // + 64: the leader kernel reads up to 2*D list entries past an image's RoIs
+    w.list = c.take<int>(static_cast<size_t>(N + 1) * R + 64);
     w.cnt = c.take<int>(N + 1);
     w.bytes = c.used();
     return w;
@@ -1363,13 +1630,15 @@ BwdWs carve_bwd(void* ws, int64_t R, int N, int PH, int PW) {
     BwdWs w{};
     w.cmask = c.take<uint64_t>(static_cast<size_t>(R) * PH * PW);
     w.code = c.take<uint8_t>(static_cast<size_t>(R) * PH * PW);
-    w.list = c.take<int>(static_cast<size_t>(N + 1) * R);
+    // + 64: the leader kernel reads up to 2*D list entries past an image's RoIs
+    w.list = c.take<int>(static_cast<size_t>(N + 1) * R + 64);
     w.cnt = c.take<int>(N + 1);
     w.bytes = c.used();
     return w;
 }
 constexpr size_t kPlaneBudget = 64 * 1024;       // LDS per workgroup for planes (plain kernel)
 constexpr int kBwdRing = 8;                      // RoIs in flight per wave (ring kernel)
+constexpr int kBwdLead = 6;                      // RoIs per step (leader kernel)
 constexpr size_t kPlaneBudgetRing = 144 * 1024;  // ring kernel: one workgroup per CU
 }  // namespace
 
@@ -1407,7 +1676,8 @@ extern "C" int frcnn_roi_pool_bwd(const float* grad, const float* rois, const in
     FRCNN_LAUNCH_CHECK("roi_lists_kernel");
     const size_t plane_bytes = HW * sizeof(float);
     const int PHW = PH * PW;
-    const bool ring = PHW <= 64 && path_cfg().roi_bwd != kPathPlain;
+    const int bp = path_cfg().roi_bwd;
+    const bool ring = PHW <= 64 && bp != kPathPlain;
     if (ring && plane_bytes <= kPlaneBudgetRing) {
         // Every wave owns one (image, channel) plane and walks all of the
         // image's RoIs, so the work per wave is fixed: spread the N*C waves
@@ -1422,9 +1692,17 @@ extern "C" int frcnn_roi_pool_bwd(const float* grad, const float* rois, const in
         cpw = cpw < 1 ? 1 : cpw;
         const int icpw = static_cast<int>(cpw);
         dim3 grid((C + icpw - 1) / icpw, N);
-        hipLaunchKernelGGL(roi_pool_bwd_pf_kernel<kBwdRing>, grid, dim3(64 * icpw), icpw * plane_bytes, st,
-                           grad, argmax, w.cmask, w.code, w.list, w.cnt, static_cast<int>(R), C,
-                           static_cast<int>(HW), PHW, PW, icpw, grad_in);
+        const bool fits = static_cast<uint64_t>(R) * C * PHW * 4 < (1ull << 31);
+        const int HWs = static_cast<int>((HW + 64 + 3) & ~static_cast<size_t>(3));  // + dummy words
+        const size_t lead_bytes = static_cast<size_t>(icpw) * (HWs * sizeof(float) + 2 * kBwdXRow * 8);
+        if (fits && bp == kPathAuto && PHW < 64 && PW == 7 && lead_bytes <= kPlaneBudgetRing)
+            hipLaunchKernelGGL((roi_pool_bwd_lead_kernel<kBwdLead, 7>), grid, dim3(64 * icpw), lead_bytes,
+                               st, grad, argmax, w.cmask, w.code, w.list, w.cnt, static_cast<int>(R), C,
+                               static_cast<int>(HW), HWs, PHW, icpw, grad_in);
+        else
+            hipLaunchKernelGGL(roi_pool_bwd_pf_kernel<kBwdRing>, grid, dim3(64 * icpw), icpw * plane_bytes, st,
+                               grad, argmax, w.cmask, w.code, w.list, w.cnt, static_cast<int>(R), C,
+                               static_cast<int>(HW), PHW, PW, icpw, grad_in);
     } else if (plane_bytes <= kPlaneBudget) {
         int cpw = static_cast<int>(kPlaneBudget / plane_bytes);
         cpw = cpw > 16 ? 16 : cpw;

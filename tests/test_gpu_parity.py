@@ -465,10 +465,12 @@ def test_roi_pool_head_fused(case):
     assert np.array_equal(xt.grad.cpu().numpy(), og)
 
 
-def test_roi_pool_bwd_ring_equals_plain():
-    """The latency-hidden backward (8-RoI load ring) and the plain plane-owner
-    kernel give identical bits, incl. duplicated RoIs (same argmax pixels across
-    RoIs and bins), images with 0 / fewer than 8 / 8k+r RoIs."""
+@pytest.mark.parametrize("path", ["auto", "ring"])
+def test_roi_pool_bwd_ring_equals_plain(path):
+    """The latency-hidden backwards (the leader-gather kernel -- the default
+    for 7-wide outputs -- and the RoI-at-a-time ring) and the plain
+    plane-owner kernel give identical bits, incl. duplicated RoIs (same argmax
+    pixels across RoIs and bins), images with 0 / fewer than 6 / 6k+r RoIs."""
     from replication_faster_rcnn_amd.ops import _roi_pool_bwd
     r = np.random.default_rng(7)
     N, C, H, W = 4, 20, 38, 38
@@ -484,7 +486,8 @@ def test_roi_pool_bwd_ring_equals_plain():
     rois = torch.tensor(rows, dtype=torch.float32, device=DEV)
     out, am = ops.roi_pool_with_argmax(x, rois, 7)
     g = torch.randn(out.shape, device=DEV)
-    a = _roi_pool_bwd(g, rois, am, x.shape, 1.0)
+    with _lib.kernel_path("roi_pool_bwd", path):
+        a = _roi_pool_bwd(g, rois, am, x.shape, 1.0)
     with _lib.kernel_path("roi_pool_bwd", "plain"):
         b = _roi_pool_bwd(g, rois, am, x.shape, 1.0)
     assert torch.equal(a, b)
@@ -492,7 +495,8 @@ def test_roi_pool_bwd_ring_equals_plain():
     assert np.array_equal(a.cpu().numpy(), ref)
 
 
-def test_roi_pool_bwd_denormal_and_colliding_grads():
+@pytest.mark.parametrize("path", ["auto", "ring", "plain"])
+def test_roi_pool_bwd_denormal_and_colliding_grads(path):
     """The backward's LDS adds keep IEEE semantics: denormal gradients and sums
     (no flush to zero), many same-pixel contributions (tiny RoIs whose 49 bins
     share a few pixels), signed zeros -- bit-identical to the CPU order."""
@@ -509,7 +513,8 @@ def test_roi_pool_bwd_denormal_and_colliding_grads():
     g = (g * scale).astype(np.float32)
     g[r.random(g.shape) < 0.05] = -0.0
     assert (np.abs(g[g != 0]) < np.finfo(np.float32).tiny).any()
-    gi = _roi_pool_bwd(torch.from_numpy(g).to(DEV), rois, am, x.shape, 1.0)
+    with _lib.kernel_path("roi_pool_bwd", path):
+        gi = _roi_pool_bwd(torch.from_numpy(g).to(DEV), rois, am, x.shape, 1.0)
     ref = orc.roi_pool_backward(g, rois.cpu().numpy(), am.cpu().numpy(), x.shape)
     assert np.array_equal(gi.cpu().numpy().view(np.uint32), ref.view(np.uint32))
 

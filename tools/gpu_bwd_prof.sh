@@ -15,4 +15,4 @@ for r in csv.DictReader(open(sys.argv[1])):
     print(r["Name"][:80].ljust(80), r["Calls"], "%.1f us"%(float(r["AverageNs"])/1e3))
 PY
 bash tools/pmc_roi_pool.sh "$OUT/pmc" bench cfg5 && \
-    python3 tools/summarize_pmc.py "$OUT/pmc" roi_pool_bwd_pf --config cfg5 --json "$OUT/roi_pool_bwd_traffic.json" > "$OUT/pmc_bwd.txt" && cat "$OUT/pmc_bwd.txt"
+    python3 tools/summarize_pmc.py "$OUT/pmc" ${KERNEL:-roi_pool_bwd_lead} --config cfg5 --json "$OUT/roi_pool_bwd_traffic.json" > "$OUT/pmc_bwd.txt" && cat "$OUT/pmc_bwd.txt"
