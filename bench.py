@@ -687,7 +687,7 @@ def main():
                    "devices": min(world, ndev)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "roi_pool_bwd_pf_kernel" if train else "roi_pool_fwd_wave_kernel<head>",
+                     "kernel": "roi_pool_bwd_lead_kernel" if train else "roi_pool_fwd_wave_kernel<head>",
                      "kernel_us": dom_ms * 1e3, "alg_bytes_per_launch": alg_bytes,
                      "kernel_us_alone": alone_ms * 1e3,
                      "frac_alone": alg_bytes / (alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},

@@ -38,6 +38,6 @@ rc=$?
 for c in cfg2 cfg4; do
   python3 tools/summarize_pmc.py "$OUT/pmc_$c" roi_pool_fwd_wave --config $c --json "$OUT/roi_pool_fwd_traffic.json" > "$OUT/pmc_$c.txt" 2>&1
 done
-python3 tools/summarize_pmc.py "$OUT/pmc_cfg5" roi_pool_bwd_pf --config cfg5 --json "$OUT/roi_pool_bwd_traffic.json" > "$OUT/pmc_cfg5.txt" 2>&1
+python3 tools/summarize_pmc.py "$OUT/pmc_cfg5" roi_pool_bwd_lead --config cfg5 --json "$OUT/roi_pool_bwd_traffic.json" > "$OUT/pmc_cfg5.txt" 2>&1
 python3 tools/summarize_pmc.py "$OUT/pmc_cfg5" roi_pool_fwd_wave --config cfg5 --json "$OUT/roi_pool_fwd_traffic.json" >> "$OUT/pmc_cfg5.txt" 2>&1
 exit $rc
