@@ -161,7 +161,11 @@ def test_roi_pool_golden(golden):
 @pytest.mark.parametrize("N,C,H,W,R,ph", [(8, 256, 38, 63, 2400, 7), (2, 3, 9, 11, 77, 3),
                                           (1, 5, 4, 4, 40, 7), (2, 64, 50, 84, 300, 7),
                                           (16, 24, 38, 38, 2048, 7), (5, 4, 12, 12, 3, 7),
-                                          (3, 8, 16, 16, 21, 8)])
+                                          (3, 8, 16, 16, 21, 8),
+                                          # rectangular outputs: 7 wide with 9 / 5 / 1 rows
+                                          # (the leader backward), 5 wide (the ring backward)
+                                          (4, 12, 20, 24, 300, (9, 7)), (2, 6, 14, 10, 120, (5, 7)),
+                                          (2, 6, 14, 10, 90, (1, 7)), (3, 6, 16, 12, 150, (7, 5))])
 def test_roi_pool_vs_oracle(N, C, H, W, R, ph):
     r = np.random.default_rng(R)
     x = r.standard_normal((N, C, H, W), dtype=np.float32)
