@@ -884,6 +884,62 @@ __global__ __launch_bounds__(256) void roi_bwd_prep_kernel(const float* __restri
     if (k < PHW) code[static_cast<size_t>(r) * PHW + k] = static_cast<uint8_t>(nb | (slow ? 16u : 0u));
 }
 
+// roi_bwd_prep_kernel for PH*PW <= 64 (same outputs): one wave per RoI, lane =
+// bin.  Bin windows are separable (rows depend on ph only, columns on pw only),
+// so a bin's overlap set is (rows overlapping its row) x (columns overlapping
+// its column): PH + PW lane reads instead of a walk over every earlier bin.
+__global__ __launch_bounds__(256) void roi_bwd_prep64_kernel(const float* __restrict__ rois, int R,
+                                                             int H, int W, int PH, int PW, float ss,
+                                                             uint64_t* __restrict__ cmask,
+                                                             uint8_t* __restrict__ code) {
+    const int lane = threadIdx.x & 63;
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= R) return;  // whole wave
+    const int PHW = PH * PW;
+    const float* roi = rois + static_cast<size_t>(r) * 5;
+    const int k = lane < PHW ? lane : 0;
+    const int pw = k % PW;
+    const int4 g = roi_bin(roi, ss, H, W, PH, PW, k / PW, pw);
+    const bool ne = lane < PHW && g.y > g.x && g.w > g.z;
+    uint64_t colbits = 0;  // columns q whose (non-empty) range overlaps this bin's
+    for (int q = 0; q < PW; ++q) {
+        const int qz = __shfl(g.z, q, 64), qw = __shfl(g.w, q, 64);  // bin (0, q)
+        if (qw > qz && qz < g.w && g.z < qw) colbits |= 1ull << q;
+    }
+    uint64_t m = 0;
+    for (int q = 0; q < PH; ++q) {
+        const int qx = __shfl(g.x, q * PW, 64), qy = __shfl(g.y, q * PW, 64);  // bin (q, 0)
+        if (qy > qx && qx < g.y && g.x < qy) m |= colbits << (q * PW);
+    }
+    m &= (1ull << lane) - 1;  // earlier bins only
+    m = ne ? m : 0ull;
+    uint32_t nb = 0;
+    bool other = false;
+    if (lane < PHW) {
+        cmask[static_cast<size_t>(r) * PHW + lane] = m;
+        uint64_t known = 0;
+        if (pw > 0) {
+            known |= 1ull << (lane - 1);
+            nb |= (m >> (lane - 1)) & 1u;
+        }
+        if (lane >= PW) {
+            known |= 1ull << (lane - PW);
+            nb |= ((m >> (lane - PW)) & 1u) << 1;
+            if (pw > 0) {
+                known |= 1ull << (lane - PW - 1);
+                nb |= ((m >> (lane - PW - 1)) & 1u) << 2;
+            }
+            if (pw < PW - 1) {
+                known |= 1ull << (lane - PW + 1);
+                nb |= ((m >> (lane - PW + 1)) & 1u) << 3;
+            }
+        }
+        other = (m & ~known) != 0;
+    }
+    const bool slow = __ballot(other) != 0;
+    if (lane < PHW) code[static_cast<size_t>(r) * PHW + lane] = static_cast<uint8_t>(nb | (slow ? 16u : 0u));
+}
+
 // General plane-owner backward (any output size; planes in LDS or, when a
 // plane does not fit, in grad_in itself with agent-scope load/store rounds).
 template <bool IN_LDS>
@@ -1668,8 +1724,12 @@ extern "C" int frcnn_roi_pool_bwd(const float* grad, const float* rois, const in
     FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_bwd: workspace %zu < %zu",
                   ws_bytes, w.bytes);
     FRCNN_REQUIRE(N <= 65535, "frcnn_roi_pool_bwd: N > 65535");
-    hipLaunchKernelGGL(roi_bwd_prep_kernel, dim3(static_cast<unsigned>(R)), dim3(256), 0, st, rois,
-                       H, W, PH, PW, spatial_scale, w.cmask, w.code);
+    if (PH * PW <= 64)
+        hipLaunchKernelGGL(roi_bwd_prep64_kernel, dim3(static_cast<unsigned>((R + 3) / 4)), dim3(256), 0, st,
+                           rois, static_cast<int>(R), H, W, PH, PW, spatial_scale, w.cmask, w.code);
+    else
+        hipLaunchKernelGGL(roi_bwd_prep_kernel, dim3(static_cast<unsigned>(R)), dim3(256), 0, st, rois,
+                           H, W, PH, PW, spatial_scale, w.cmask, w.code);
     FRCNN_LAUNCH_CHECK("roi_bwd_prep_kernel");
     hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, rois, static_cast<int>(R),
                        N, w.list, w.cnt);

@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py \
-    -k "bwd" > "$OUT/pytest.log" 2>&1
+    -k "bwd or vs_oracle or golden" > "$OUT/pytest.log" 2>&1
 rc=$?; tail -2 "$OUT/pytest.log"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python3 tools/ab_roi_pool_bwd.py --paths "$PATHS" --rounds 7 > "$OUT/ab.json" 2>&1
 rc=$?; cat "$OUT/ab.json"; [ $rc -eq 0 ] || exit $rc
