@@ -4,13 +4,16 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <cstring>
+#include <mutex>
 
 #include "common.h"
 
 namespace frcnn {
 
 static thread_local char g_err[512] = "";
+constexpr int kMaxDevices = 64;
 
 void set_error(const char* fmt, ...) {
     va_list ap;
@@ -33,16 +36,22 @@ static PathCfg g_path;
 const PathCfg& path_cfg() { return g_path; }
 
 int device_cu_count() {
-    static int cus = 0;
-    if (cus <= 0) {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-            cus = n;
-        else
-            cus = 256;
+    // per device (a process may drive several GPUs, one per thread)
+    static std::atomic<int> cus[kMaxDevices] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) {
+        (void)hipGetLastError();
+        return 256;
     }
-    return cus;
+    int n = cus[dev].load(std::memory_order_relaxed);
+    if (n <= 0) {
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) {
+            (void)hipGetLastError();
+            n = 256;
+        }
+        cus[dev].store(n, std::memory_order_relaxed);
+    }
+    return n;
 }
 
 }  // namespace frcnn
@@ -57,9 +66,11 @@ extern "C" int frcnn_set_path(const char* op, const char* path) {
     }
     auto is = [&](const char* a, const char* b) { return std::strcmp(a, b) == 0; };
     const bool aut = is(path, "auto");
-    if (is(op, "roi_pool_fwd") && (aut || is(path, "wave") || is(path, "dense") || is(path, "generic"))) {
+    if (is(op, "roi_pool_fwd") &&
+        (aut || is(path, "pair") || is(path, "wave") || is(path, "dense") || is(path, "generic"))) {
         g_path.roi_fwd = aut ? kPathAuto : is(path, "generic") ? kPathGeneric
                                        : is(path, "dense")     ? kPathDense
+                                       : is(path, "pair")      ? kPathPair
                                                                : kPathWave;
     } else if (is(op, "roi_pool_bwd") &&
                (aut || is(path, "ring") || is(path, "plain"))) {
@@ -123,8 +134,30 @@ extern "C" int frcnn_stream_create(const uint32_t* cu_mask, int words, void** ou
     return FRCNN_OK;
 }
 
+namespace frcnn {
+// CU counts of streams, keyed by (device, handle): a stream's CU mask is fixed
+// at creation, and frcnn_stream_destroy evicts its entry, so a later stream
+// that reuses the handle value is looked up afresh.
+struct CuCache {
+    std::mutex mu;
+    hipStream_t s[16] = {};
+    int dev[16] = {};
+    int n[16] = {};
+    int next = 0;
+};
+static CuCache g_cu_cache;
+
+static void cu_cache_evict(hipStream_t st) {
+    std::lock_guard<std::mutex> lk(g_cu_cache.mu);
+    for (int i = 0; i < 16; ++i)
+        if (g_cu_cache.s[i] == st) g_cu_cache.s[i] = nullptr;
+}
+}  // namespace frcnn
+
 extern "C" int frcnn_stream_destroy(void* stream) {
-    if (stream && hipStreamDestroy(frcnn::as_stream(stream)) != hipSuccess)
+    if (!stream) return FRCNN_OK;
+    frcnn::cu_cache_evict(frcnn::as_stream(stream));
+    if (hipStreamDestroy(frcnn::as_stream(stream)) != hipSuccess)
         return frcnn::check_launch("frcnn_stream_destroy");
     return FRCNN_OK;
 }
@@ -136,11 +169,13 @@ namespace frcnn {
 int stream_cu_count(hipStream_t s) {
     const int all = device_cu_count();
     if (!s) return all;
-    static thread_local hipStream_t c_s[8] = {};
-    static thread_local int c_n[8] = {};
-    static thread_local int c_next = 0;
-    for (int i = 0; i < 8; ++i)
-        if (c_s[i] == s) return c_n[i];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    {
+        std::lock_guard<std::mutex> lk(g_cu_cache.mu);
+        for (int i = 0; i < 16; ++i)
+            if (g_cu_cache.s[i] == s && g_cu_cache.dev[i] == dev) return g_cu_cache.n[i];
+    }
     uint32_t m[32] = {};
     int n = all;
     if (hipExtStreamGetCUMask(s, 32, m) == hipSuccess) {
@@ -150,9 +185,12 @@ int stream_cu_count(hipStream_t s) {
     } else {
         (void)hipGetLastError();
     }
-    c_s[c_next] = s;
-    c_n[c_next] = n;
-    c_next = (c_next + 1) & 7;
+    std::lock_guard<std::mutex> lk(g_cu_cache.mu);
+    const int i = g_cu_cache.next;
+    g_cu_cache.s[i] = s;
+    g_cu_cache.dev[i] = dev;
+    g_cu_cache.n[i] = n;
+    g_cu_cache.next = (i + 1) & 15;
     return n;
 }
 }  // namespace frcnn

@@ -750,6 +750,241 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
     PPROF_T(3);
 }
 
+// ------------------------------------------------- pair-tile forward
+// The default forward for RoIs grouped by image when the tiles fit the CU's
+// LDS.  Same grid and RoI shares as the wave kernel, but the workgroup stages
+// TWO tiles of its CG channel planes: the raw pixels and the horizontal pixel
+// PAIRS -- pair (h, w) = the first maximum of pixels (h, w), (h, w+1) under
+// torchvision's strict '>' (NaN never selected), plus one flag bit per channel
+// saying whether it is the second pixel.  A lane (= one bin) scans each window
+// row as pairs at columns ws, ws+2, ..., the last one clamped to we-2 (a pair
+// seen twice can never pass the strict '>' again); 1-wide windows read the raw
+// tile.  Scanning pairs in row-major order picks the same first maximum as
+// scanning pixels: the first pair holding the overall maximum holds its first
+// occurrence, and a tie inside the pair goes to its first pixel.  So a window
+// row of width w takes ceil(w/2) updates instead of w, each the same compare +
+// two selects per channel; the update records X = (pair pixel << 16) | flags
+// and the argmax is decoded once after the scan (pixel + this channel's flag).
+// Staging the pairs costs one compare per pixel-channel per workgroup against
+// ~47 window visits of each pixel-channel at cfg2.
+// Lanes: one bin each; for the 7x7 head the lane -> bin map puts two whole
+// bin rows into each of the four 16-lane groups a ds_read_b128 is serviced in
+// (fewer bank conflicts than consecutive bins: rows of one bin row share the
+// pixel row).  Waves pull RoIs from an LDS counter; the chunk prologue
+// computes each RoI's geometry once per workgroup, with its largest bin height
+// and pair count (the wave-uniform loop bounds).
+__constant__ signed char kPairLaneBin7[64] = {
+    0,  1,  2,  3,  14, 15, 16, 17, 18, 19, 20, 21, 4,  5,  6,  7,  22, 23, 24, 25, 8,  9,
+    10, 11, 12, 13, -1, -1, 26, 27, -1, -1, 28, 29, 30, 31, 42, 43, 44, 45, 46, 47, 48, -1,
+    32, 33, 34, 35, -1, -1, -1, -1, 36, 37, 38, 39, 40, 41, -1, -1, -1, -1, -1, -1};
+
+__host__ __device__ constexpr int pair_hws(int HW) { return (HW + 16) & ~15; }  // + the sentinel pixel HW
+
+template <int NT, int CG, int FIX, bool HEAD>
+__global__ __launch_bounds__(NT) void roi_pool_fwd_pair_kernel(
+    const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W, int PH_, int PW_,
+    float ss, float* __restrict__ out, int32_t* __restrict__ argmax, int geo_cap, HeadArgs hd) {
+    const int PH = FIX ? FIX : PH_, PW = FIX ? FIX : PW_;
+    constexpr int NP = CG / 4;
+    static_assert(CG <= 8, "8 flag bits per pixel word");
+    extern __shared__ __attribute__((aligned(16))) float4 q4[];
+    __shared__ int s_red[2 * (NT / 64)];
+    __shared__ int s_next;
+    const int b = blockIdx.z;
+    const int c0 = blockIdx.x * CG;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int HW = H * W;
+    const int HWs = pair_hws(HW);
+    const int PHW = PH * PW;
+    const int split = gridDim.y, z = blockIdx.y;
+    const int N = gridDim.z - 1;
+    if (b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
+        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, 0, N, s_red, 1)
+                             : roi_range_sorted<NT>(rois, R, 0, N, s_red);
+        const int n_lo = rg.x, tot = n_lo + (R - rg.y);
+        const int lo = static_cast<int>(static_cast<int64_t>(tot) * z / split);
+        const int hi = static_cast<int>(static_cast<int64_t>(tot) * (z + 1) / split);
+        if (HEAD && hd.boxes && blockIdx.x == 0)
+            for (int t = lo + tid; t < hi; t += NT) {
+                const int r = t < n_lo ? t : rg.y + (t - n_lo);
+                float bx[5];
+                head_box(rois, hd, r, bx);
+#pragma unroll
+                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
+            }
+        for (int e = lo * CG * PHW + tid; e < hi * CG * PHW; e += NT) {
+            const int t = e / (CG * PHW);
+            const int rem = e - t * (CG * PHW);
+            const int r = t < n_lo ? t : rg.y + (t - n_lo);
+            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + rem;
+            out[o] = 0.0f;
+            argmax[o] = -1;
+        }
+        return;
+    }
+    const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, b, b + 1, s_red, 1)
+                         : roi_range_sorted<NT>(rois, R, b, b + 1, s_red);
+    const int rbase = rg.x, nr = rg.y - rg.x;
+    if (z >= nr) return;
+    const int nmine = (nr - z + split - 1) / split;  // items z, z+split, ...
+    // ---- LDS: raw planes | pair planes | flags | RoI geometry | loop bounds
+    float4* raw = q4;
+    float4* prt = q4 + NP * HWs;
+    uint16_t* flw = reinterpret_cast<uint16_t*>(q4 + 2 * NP * HWs);
+    int4* s_geo = reinterpret_cast<int4*>(flw + HWs);  // HWs is a multiple of 16
+    int* s_ext = reinterpret_cast<int*>(s_geo + geo_cap);
+    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+    for (int p = tid; p < HW; p += NT) {
+        float v[CG];
+#pragma unroll
+        for (int q = 0; q < CG; ++q) v[q] = src[static_cast<size_t>(q) * HW + p];
+#pragma unroll
+        for (int k = 0; k < NP; ++k) raw[k * HWs + p] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    }
+    for (int p = HW + tid; p < HWs; p += NT)  // the sentinel pixel HW and the padding: -inf
+#pragma unroll
+        for (int k = 0; k < NP; ++k) raw[k * HWs + p] = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    __syncthreads();
+    // pairs + flag words: flw[p] = (w << 8) | flags (bit c: channel c's pair
+    // maximum is the second pixel), so a scan step's index record is its row's
+    // (h * W) << 8 plus this word; the sentinel's word is 0
+    for (int p = tid; p < HWs; p += NT) {
+        const int row = p / W;
+        const int w = p - row * W;
+        const bool two = p < HW && w != W - 1;  // pixel (h, w+1) exists
+        uint32_t fl = 0;
+#pragma unroll
+        for (int k = 0; k < NP; ++k) {
+            const float4 a4 = raw[k * HWs + p];
+            const float4 b4 = raw[k * HWs + (two ? p + 1 : p)];
+            const float a[4] = {a4.x, a4.y, a4.z, a4.w};
+            const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
+            float o[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                // the pixel a strict-'>' scan of (a, b) from -FLT_MAX keeps: b iff
+                // b > a, or a is NaN (never selected) -- then b, NaN or not
+                const bool tb = two && (bb[j] > a[j] || a[j] != a[j]);
+                o[j] = tb ? bb[j] : a[j];
+                fl |= static_cast<uint32_t>(tb) << (4 * k + j);
+            }
+            prt[k * HWs + p] = make_float4(o[0], o[1], o[2], o[3]);
+        }
+        flw[p] = static_cast<uint16_t>(p < HW ? (w << 8) | fl : 0);
+    }
+    const int bin = FIX == 7 ? static_cast<int>(kPairLaneBin7[lane]) : (lane < PHW ? lane : -1);
+    const bool act = bin >= 0;
+    const int ph = act ? bin / PW : 0, pw = act ? bin - (bin / PW) * PW : 0;
+    const char* tb = reinterpret_cast<const char*>(q4);  // byte offsets below
+    const uint32_t plane_bytes = static_cast<uint32_t>(HWs) * 16u;
+    const uint32_t raw_b = 0, prt_b = NP * plane_bytes, flw_b = 2 * NP * plane_bytes;
+    for (int k0 = 0; k0 < nmine; k0 += geo_cap) {
+        const int cn = min(geo_cap, nmine - k0);
+        for (int i = tid; i < cn; i += NT) {
+            const int r = rbase + z + (k0 + i) * split;
+            float bx[5];
+            if (HEAD) {
+                head_box(rois, hd, r, bx);
+                if (hd.boxes && blockIdx.x == 0) {
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 5; ++j) bx[j] = rois[static_cast<size_t>(r) * 5 + j];
+            }
+            const RoiGeom gm = roi_geom(bx, ss, PH, PW);
+            s_geo[i] = make_int4(gm.sh, gm.sw, __float_as_int(gm.bh), __float_as_int(gm.bw));
+            // wave-uniform loop bounds: the largest bin height and pair count
+            int hm = 0, um = 0;
+            for (int q = 0; q < PH; ++q) {
+                const int4 g = geom_bin(gm, H, W, q, 0);
+                hm = max(hm, g.y - g.x);
+            }
+            for (int q = 0; q < PW; ++q) {
+                const int4 g = geom_bin(gm, H, W, 0, q);
+                const int w = g.w - g.z;
+                um = max(um, w <= 0 ? 0 : (w == 1 ? 1 : (w + 1) >> 1));
+            }
+            s_ext[i] = (hm << 16) | um;
+        }
+        if (tid == 0) s_next = 0;
+        __syncthreads();  // tiles staged (first chunk) / geometry of the chunk
+        int k = 0;
+        if (lane == 0) k = atomicAdd(&s_next, 1);
+        k = __builtin_amdgcn_readfirstlane(k);
+        while (k < cn) {
+            int kn = 0;
+            if (lane == 0) kn = atomicAdd(&s_next, 1);  // prefetch the next item
+            const int r = rbase + z + (k0 + k) * split;
+            const int4 gq = s_geo[k];
+            const int ext = __builtin_amdgcn_readfirstlane(s_ext[k]);
+            const int Hm = ext >> 16, Um = ext & 0xffff;
+            RoiGeom gm;
+            gm.sh = gq.x;
+            gm.sw = gq.y;
+            gm.bh = __int_as_float(gq.z);
+            gm.bw = __int_as_float(gq.w);
+            const int4 g = geom_bin(gm, H, W, ph, pw);
+            const int ww = g.w - g.z;
+            const bool empty = !act || g.y <= g.x || ww <= 0;
+            const int hh = empty ? 0 : g.y - g.x;
+            const bool single = ww == 1;
+            const int last = max(ww - 2, 0);  // start of a row's last pair (0: 1-wide, raw tile)
+            const uint32_t tbase = single ? raw_b : prt_b;
+            float m[CG];
+            int X[CG];
+#pragma unroll
+            for (int c = 0; c < CG; ++c) {
+                m[c] = empty ? 0.0f : -FLT_MAX;
+                X[c] = static_cast<int>(0xFFFFFF00u);  // decodes to -1
+            }
+            int rowpix = g.x * W + g.z;
+            for (int i = 0; i < Hm; ++i) {
+                if (i < hh) {
+                    const uint32_t ra0 = tbase + static_cast<uint32_t>(rowpix) * 16u;
+                    const uint32_t ra1 = ra0 + plane_bytes;
+                    // 1-wide windows read the sentinel's word 0: their one pixel is "first"
+                    const uint32_t fra = flw_b + 2u * static_cast<uint32_t>(single ? HW : rowpix);
+                    const int rowX = (rowpix - g.z) << 8;  // (h * W) << 8
+                    const int rowXs = single ? (rowpix << 8) : rowX;
+                    for (int j = 0; j < Um; ++j) {
+                        const uint32_t q = static_cast<uint32_t>(min(2 * j, last));
+                        const float4 v0 = *static_cast<const float4*>(__builtin_assume_aligned(tb + ra0 + q * 16u, 16));
+                        float4 v1 = v0;
+                        if (NP > 1) v1 = *static_cast<const float4*>(__builtin_assume_aligned(tb + ra1 + q * 16u, 16));
+                        const uint32_t fw = *reinterpret_cast<const uint16_t*>(tb + fra + 2u * q);
+                        // every read in flight before the first compare
+                        __builtin_amdgcn_sched_barrier(0);
+                        const int xn = rowXs + static_cast<int>(fw);
+                        const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+                        for (int c = 0; c < CG; ++c) {
+                            if (vv[c] > m[c]) {  // torchvision's strict '>'
+                                m[c] = vv[c];
+                                X[c] = xn;
+                            }
+                        }
+                    }
+                }
+                rowpix += W;
+            }
+            if (act) {
+                const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + bin;
+                float* op = out + o;
+                int32_t* ap = argmax + o;
+#pragma unroll
+                for (int c = 0; c < CG; ++c) {
+                    op[c * PHW] = m[c];
+                    ap[c * PHW] = (X[c] >> 8) + ((X[c] >> c) & 1);
+                }
+            }
+            k = __builtin_amdgcn_readfirstlane(kn);
+        }
+        __syncthreads();  // the chunk's geometry and s_next are reused
+    }
+}
+
 // nets/heads.py:42-47 (fp32 divide, then multiply) + [idx, box] pack.
 __global__ __launch_bounds__(256) void roi_transform_kernel(const float* __restrict__ rois,
                                                             const float* __restrict__ inds,
@@ -1231,12 +1466,13 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
         int am_r[D];
         float g_r[D];
         uint32_t cd_r[D], cl_r[D], ch_r[D];
-        // list entries past the image's RoIs (the workspace is padded) are
-        // garbage: their slots are dead (argmax -1) and the buffer loads are
-        // range-checked
+        // list positions past the image's RoIs re-read its last RoI (scalar
+        // clamp): the workspace tail is never written, and a raw buffer load's
+        // soffset is not range-checked, so a stale entry could address far
+        // past the buffers; those slots are dead (argmax -1)
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            const int n = lst[d];
+            const int n = lst[d < nr ? d : nr - 1];
             const uint32_t so = static_cast<uint32_t>(n) * rpb + cpb;
             const uint32_t sm = static_cast<uint32_t>(n) * PHW;
             am_r[d] = __builtin_amdgcn_raw_buffer_load_b32(rs_a, kl * 4, so, 0);
@@ -1252,7 +1488,10 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
             const unsigned long long p0 = BPROF_T();
             int nx[D];
 #pragma unroll
-            for (int d = 0; d < D; ++d) nx[d] = lst[t0 + D + d];
+            for (int d = 0; d < D; ++d) {
+                const int tn = t0 + D + d;
+                nx[d] = lst[tn < nr ? tn : nr - 1];
+            }
             int am[D], addr[D];
             float g[D], s1[D], s3[D], s4[D];
             bool slow[D];
@@ -1455,7 +1694,7 @@ struct FwdWs {
 FwdWs carve_fwd(void* ws, int64_t R, int N) {
     Carver c(ws);
     FwdWs w{};
-    // + 64: the leader kernel reads up to 2*D list entries past an image's RoIs
+    // + 64: slack (kernels clamp list reads to each image's count)
     w.list = c.take<int>(static_cast<size_t>(N + 1) * R + 64);
     w.cnt = c.take<int>(N + 1);
     w.bytes = c.used();
@@ -1516,6 +1755,57 @@ int px_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, in
     }
 #undef FRCNN_PX
     FRCNN_LAUNCH_CHECK("roi_pool_fwd_wave_kernel");
+    return FRCNN_OK;
+}
+
+// Launch plan of the pair-tile forward: CG = 8 channel planes when the raw +
+// pair tiles (+ flags) fit the CU's LDS with room for a RoI-geometry chunk,
+// else 4; split as the wave kernel (one grid slot per resident workgroup of
+// the launch stream's CUs).  CG = 0: does not fit (the wave kernel runs).
+PxPlan pair_plan(int C, int N, int H, int W, int PHW, hipStream_t st) {
+    PxPlan pl;
+    const size_t HW = static_cast<size_t>(H) * W;
+    if (N <= 0 || HW == 0 || PHW > 64 || W > 255 || HW + 16 > (1 << 22)) return pl;  // flag word: w in 8 bits
+    constexpr size_t kReserve = 256;  // static LDS (s_red, s_next) + allocation rounding
+    constexpr size_t kPerGeo = sizeof(int4) + sizeof(int);
+    constexpr size_t kMinGeo = 64 * kPerGeo;
+    const size_t HWs = static_cast<size_t>(pair_hws(static_cast<int>(HW)));
+    for (int cg : {8, 4}) {
+        if (C % cg != 0) continue;
+        if (path_cfg().roi_cg && cg != path_cfg().roi_cg) continue;  // A/B override
+        const size_t tile = 2 * static_cast<size_t>(cg / 4) * HWs * sizeof(float4) + HWs * sizeof(uint16_t);
+        int per_cu = 0;
+        if (2 * (tile + kMinGeo + kReserve) <= kLdsPerCu) per_cu = 2;
+        else if (tile + kMinGeo + kReserve <= kLdsPerCu) per_cu = 1;
+        if (!per_cu) continue;
+        const size_t geo = (kLdsPerCu / per_cu - kReserve - tile) / kPerGeo;
+        pl.geo_cap = static_cast<int>(geo > 512 ? 512 : geo);
+        pl.cg = cg;
+        pl.lds = tile + static_cast<size_t>(pl.geo_cap) * kPerGeo;
+        const int64_t wgs = static_cast<int64_t>(C / cg) * N;
+        int64_t sp = (static_cast<int64_t>(stream_cu_count(st)) * per_cu + wgs - 1) / wgs;
+        if (path_cfg().roi_split > 0) sp = path_cfg().roi_split;  // A/B override
+        pl.split = static_cast<int>(sp < 1 ? 1 : (sp > 64 ? 64 : sp));
+        return pl;
+    }
+    return pl;
+}
+
+template <bool HEAD>
+int pair_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
+                int PH, int PW, float ss, float* out, int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
+    const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(pl.split), static_cast<unsigned>(N + 1));
+    const bool fix7 = PH == 7 && PW == 7;
+#define FRCNN_PR(CG, FX)                                                                                     \
+    hipLaunchKernelGGL((roi_pool_fwd_pair_kernel<1024, CG, FX, HEAD>), grid, dim3(1024), pl.lds, st, x, rois, \
+                       static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd)
+    if (pl.cg == 8) {
+        if (fix7) FRCNN_PR(8, 7); else FRCNN_PR(8, 0);
+    } else {
+        if (fix7) FRCNN_PR(4, 7); else FRCNN_PR(4, 0);
+    }
+#undef FRCNN_PR
+    FRCNN_LAUNCH_CHECK("roi_pool_fwd_pair_kernel");
     return FRCNN_OK;
 }
 
@@ -1598,8 +1888,13 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
     FRCNN_REQUIRE(x && rois && out && argmax, "frcnn_roi_pool_fwd: null pointer");
     hipStream_t st = as_stream(stream);
     const int path = path_cfg().roi_fwd;
-    const PxPlan xp = (rois_sorted && (path == kPathAuto || path == kPathWave)) ? px_plan(C, N, H, W, PH * PW, st)
-                                                                              : PxPlan{};
+    const PxPlan pp = (rois_sorted && (path == kPathAuto || path == kPathPair)) ? pair_plan(C, N, H, W, PH * PW, st)
+                                                                               : PxPlan{};
+    if (pp.cg)
+        return pair_launch<false>(pp, x, rois, R, N, C, H, W, PH, PW, spatial_scale, out, argmax, HeadArgs{}, st);
+    const PxPlan xp = (rois_sorted && (path == kPathAuto || path == kPathWave || path == kPathPair))
+                          ? px_plan(C, N, H, W, PH * PW, st)
+                          : PxPlan{};
     if (xp.cg)
         return px_launch<false>(xp, x, rois, R, N, C, H, W, PH, PW, spatial_scale, out, argmax, HeadArgs{}, st);
     const DensePlan pl = path == kPathGeneric ? DensePlan{} : dense_plan(C, N, H, W, PH * PW);
@@ -1648,7 +1943,16 @@ extern "C" int frcnn_roi_pool_fwd_head(const float* x, const float* rois, const 
     FRCNN_REQUIRE(rois && roi_inds && boxes, "frcnn_roi_pool_fwd_head: null pointer");
     const int path = path_cfg().roi_fwd;
     const bool aligned = reinterpret_cast<uintptr_t>(rois) % 16 == 0;
-    const PxPlan xp = (rois_sorted && C > 0 && aligned && (path == kPathAuto || path == kPathWave))
+    const PxPlan pp = (rois_sorted && C > 0 && aligned && (path == kPathAuto || path == kPathPair))
+                          ? pair_plan(C, N, H, W, PH * PW, as_stream(stream))
+                          : PxPlan{};
+    if (pp.cg) {  // transform + pack inside the pool kernel
+        FRCNN_REQUIRE(x && out && argmax, "frcnn_roi_pool_fwd_head: null pointer");
+        const HeadArgs hd{roi_inds, img_h, img_w, static_cast<float>(H), static_cast<float>(W), boxes};
+        return pair_launch<true>(pp, x, rois, R, N, C, H, W, PH, PW, spatial_scale, out, argmax, hd,
+                                 as_stream(stream));
+    }
+    const PxPlan xp = (rois_sorted && C > 0 && aligned && (path == kPathAuto || path == kPathWave || path == kPathPair))
                           ? px_plan(C, N, H, W, PH * PW, as_stream(stream))
                           : PxPlan{};
     if (xp.cg) {  // transform + pack inside the pool kernel
@@ -1686,7 +1990,7 @@ BwdWs carve_bwd(void* ws, int64_t R, int N, int PH, int PW) {
     BwdWs w{};
     w.cmask = c.take<uint64_t>(static_cast<size_t>(R) * PH * PW);
     w.code = c.take<uint8_t>(static_cast<size_t>(R) * PH * PW);
-    // + 64: the leader kernel reads up to 2*D list entries past an image's RoIs
+    // + 64: slack (kernels clamp list reads to each image's count)
     w.list = c.take<int>(static_cast<size_t>(N + 1) * R + 64);
     w.cnt = c.take<int>(N + 1);
     w.bytes = c.used();

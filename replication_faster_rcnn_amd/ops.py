@@ -23,7 +23,8 @@ from . import _lib
 
 
 def _to_dev(t: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
-    if t.is_cuda and t.dtype == dtype and t.is_contiguous():  # the device-resident fast path
+    # the device-resident fast path: already on the device the kernels launch on
+    if t.is_cuda and t.dtype == dtype and t.is_contiguous() and t.device.index == _lib._cur_device():
         return t
     return t.to(device=_lib.device(), dtype=dtype).contiguous()
 

@@ -541,3 +541,95 @@ def test_propose_caller_buffers():
     with pytest.raises(RuntimeError):
         ops.propose(sc, de, out=(out[0][:, :10], out[1], out[2]), **kw)
 
+
+
+def test_benched_step_cfg2_vs_oracle():
+    """The exact composition bench.py times at cfg2 (BASELINE configs[1]): the
+    batched proposal layer over 8 x 38 x 63 x 9 anchors (6000 -> 300) feeding
+    the head's transform + pack + RoIPool (roi_pool_fwd_wave_kernel<.., HEAD>,
+    rois_sorted) over all 2400 padded proposal rows, against the oracle's
+    nets/rpn.py:58-77 per image -> nets/heads.py:42-47 -> torchvision roi_pool.
+    Runs on a plain side stream: the pool sizes its shares to the launch
+    stream's CUs, as in the bench's step streams."""
+    from bench import make_inputs
+    c = synth.CONFIGS["cfg2"]
+    N, post, H, W = c["batch"], c["post_nms"], c["feat_h"], c["feat_w"]
+    _, sc, de, x = make_inputs("cfg2", range(N), torch.device(DEV))
+    base = A.generate_anchor_base_device(anchor_scales=c["scales"])
+    inds = torch.arange(N, device=DEV, dtype=torch.float32).repeat_interleave(post)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        rois, idx, cnt = ops.propose(sc, de, img_w=c["img_w"], img_h=c["img_h"], pre_nms=c["pre_nms"],
+                                     post_nms=post, anchor_base=base, feat_h=H, feat_w=W)
+        out, am, boxes = ops.roi_pool_head(x, rois.view(-1, 4), inds, 7, c["img_h"], c["img_w"],
+                                           rois_sorted=True)
+    s.synchronize()
+    anchors = orc.generate_anchors(orc.generate_anchor_base(anchor_scales=c["scales"]), 16, W, H)
+    Anc = len(anchors)
+    o_rois = np.zeros((N, post, 4), np.float32)
+    for i in range(N):
+        r_i, i_i = orc.propose_one(anchors, synth.rpn_scores(Anc, 0, i), synth.rpn_deltas(Anc, 0, i),
+                                   c["img_w"], c["img_h"], c["pre_nms"], post)
+        k = int(cnt[i])
+        assert k == len(i_i), i
+        assert np.array_equal(idx[i, :k].cpu().numpy().astype(np.int64), i_i), i
+        o_rois[i, :k] = r_i
+    assert np.array_equal(rois.cpu().numpy().view(np.uint32), o_rois.view(np.uint32))
+    oboxes = orc.roi_transform(o_rois.reshape(-1, 4), inds.cpu().numpy(), c["img_h"], c["img_w"], H, W)
+    assert np.array_equal(boxes.cpu().numpy().view(np.uint32), oboxes.view(np.uint32))
+    oo, oa = orc.roi_pool_forward(x.cpu().numpy(), oboxes, 7)
+    assert np.array_equal(am.cpu().numpy(), oa)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), oo.view(np.uint32))
+
+
+@pytest.mark.parametrize("ss", [0.5, 0.0625, 2.0])
+@pytest.mark.parametrize("sorted_", [True, False])
+def test_roi_pool_spatial_scale(ss, sorted_):
+    """spatial_scale != 1 (torchvision's roundf(roi * spatial_scale) RoI ends):
+    forward (wave / dense paths) and backward bit-exact vs the oracle.  The
+    reference itself passes 1 (nets/heads.py:8,48)."""
+    r = np.random.default_rng(int(ss * 1000) + sorted_)
+    N, C, H, W, R = 3, 16, 24, 30, 240
+    x = r.standard_normal((N, C, H, W), dtype=np.float32)
+    b = np.sort(r.integers(0, N, R)) if sorted_ else r.integers(0, N, R)
+    lim = max(H, W) / ss
+    xy = r.uniform(-3 / ss, lim, (R, 2)).astype(np.float32)
+    wh = r.uniform(0, lim, (R, 2)).astype(np.float32)
+    rois = np.concatenate([b[:, None].astype(np.float32), xy, xy + wh], 1).astype(np.float32)
+    out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7,
+                                       ss, rois_sorted=bool(sorted_))
+    oo, oa = orc.roi_pool_forward(x, rois, 7, ss)
+    assert np.array_equal(am.cpu().numpy(), oa)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), oo.view(np.uint32))
+    gr = r.standard_normal(oo.shape).astype(np.float32)
+    from replication_faster_rcnn_amd.ops import _roi_pool_bwd
+    gi = _roi_pool_bwd(torch.from_numpy(gr).to(DEV), torch.from_numpy(rois).to(DEV), am, x.shape, ss)
+    assert np.array_equal(gi.cpu().numpy(), orc.roi_pool_backward(gr, rois, oa, x.shape))
+
+
+@pytest.mark.parametrize("path", ["auto", "ring"])
+def test_roi_pool_bwd_poisoned_workspace(path):
+    """The backward's per-image RoI lists are written only up to each image's
+    count; the kernels must not read past it.  The cached workspace is filled
+    with 0x7f bytes (RoI index 0x7f7f7f7f) before the call."""
+    from replication_faster_rcnn_amd.ops import _roi_pool_bwd
+    r = np.random.default_rng(77)
+    N, C, H, W, R = 4, 8, 20, 22, 37  # image RoI counts not multiples of the ring depth
+    x = r.standard_normal((N, C, H, W), dtype=np.float32)
+    b = r.integers(0, N, R).astype(np.float32)
+    xy = r.uniform(-2, 20, (R, 2)).astype(np.float32)
+    rois = np.concatenate([b[:, None], xy, xy + r.uniform(0, 15, (R, 2)).astype(np.float32)], 1)
+    rois = rois.astype(np.float32)
+    oo, oa = orc.roi_pool_forward(x, rois, 7)
+    gr = r.standard_normal(oo.shape).astype(np.float32)
+    ref = orc.roi_pool_backward(gr, rois, oa, x.shape)
+    lib = _lib.load()
+    need = lib.frcnn_roi_pool_bwd_workspace_size(R, N, 7, 7)
+    with _lib.kernel_path("roi_pool_bwd", path):
+        ws = _lib.cached_workspace("roi_pool_bwd", need, torch.device(DEV))
+        ws.fill_(0x7f)
+        gi = _roi_pool_bwd(torch.from_numpy(gr).to(DEV), torch.from_numpy(rois).to(DEV),
+                           torch.from_numpy(oa).to(DEV), x.shape, 1.0)
+        torch.cuda.synchronize()
+    assert np.array_equal(gi.cpu().numpy(), ref)
