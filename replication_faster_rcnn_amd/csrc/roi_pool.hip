@@ -28,6 +28,8 @@
 namespace frcnn {
 
 constexpr int kMaxBins = 1024;
+constexpr int kListPad = 16;  // entries past each image's RoI list (copies of its last entry)
+__host__ __device__ constexpr int64_t list_stride(int64_t R) { return R + kListPad; }
 constexpr size_t kLdsPerCu = 160 * 1024;  // gfx950
 
 // torchvision bin window (hs, he, ws, we) of bin (ph, pw) for RoI `roi`.
@@ -279,7 +281,7 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_dense_kernel(
     const int* lst = nullptr;
     if (LIST) {
         nr = cnt[b];
-        lst = list + static_cast<size_t>(b) * R;
+        lst = list + static_cast<size_t>(b) * list_stride(R);
     } else {
         const int N = gridDim.z - 1;
         if (b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
@@ -1003,15 +1005,22 @@ __global__ __launch_bounds__(256) void roi_transform_kernel(const float* __restr
 }
 
 // Ordered per-image RoI lists: list[b][*] = RoIs with batch index b, ascending.
+// Each image's list has room for kListPad entries past its RoIs.
 // Block N (the extra one) collects the RoIs whose batch index is outside [0, N).
 // `stride`: floats between consecutive batch indices (5 for [R,5] RoIs, 1 for
 // the head's roi_inds).
+// `code` (optional, the backward prep's per-bin codes): entries of RoIs whose
+// bin 0 code has the "slow" bit (overlaps beyond the grid neighbours) get bit
+// 31 set, so the leader backward learns a RoI's path from the scalar list load.
 __global__ __launch_bounds__(1024) void roi_lists_kernel(const float* __restrict__ rois, int R,
                                                          int N, int* __restrict__ list,
-                                                         int* __restrict__ cnt, int stride = 5) {
+                                                         int* __restrict__ cnt, int stride = 5,
+                                                         const uint8_t* __restrict__ code = nullptr,
+                                                         int PHW = 0) {
     const int b = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     __shared__ int s_w[16];
+    __shared__ int s_last;
     int base = 0;
     for (int r0 = 0; r0 < R; r0 += 1024) {
         int r = r0 + tid;
@@ -1025,11 +1034,19 @@ __global__ __launch_bounds__(1024) void roi_lists_kernel(const float* __restrict
             before += w < wid ? s_w[w] : 0;
             tot += s_w[w];
         }
-        if (m) list[static_cast<size_t>(b) * R + base + before + __popcll(bal & lanemask_lt())] = r;
+        if (m) {
+            const int flag = code ? (code[static_cast<size_t>(r) * PHW] & 16) << 27 : 0;
+            const int pos = base + before + __popcll(bal & lanemask_lt());
+            list[static_cast<size_t>(b) * list_stride(R) + pos] = r | flag;
+            if (pos == base + tot - 1) s_last = r | flag;
+        }
         base += tot;
         __syncthreads();
     }
     if (tid == 0) cnt[b] = base;
+    // kListPad entries past the last one repeat it, so a reader may fetch whole
+    // groups of entries past the image's count without bounds checks
+    if (tid < kListPad) list[static_cast<size_t>(b) * list_stride(R) + base + tid] = base > 0 ? s_last : 0;
 }
 
 // Outputs of RoIs with an out-of-range batch index: 0 / -1 (torchvision: UB);
@@ -1043,7 +1060,7 @@ __global__ __launch_bounds__(256) void roi_pool_invalid_fill_kernel(const int* _
                                                                     HeadArgs hd = HeadArgs{}) {
     const int n = cnt[N];
     for (int t = blockIdx.x; t < n; t += gridDim.x) {
-        const int r = list[static_cast<size_t>(N) * R + t];
+        const int r = list[static_cast<size_t>(N) * list_stride(R) + t];
         const size_t base = static_cast<size_t>(r) * per_roi;
         if (hd.inds && threadIdx.x == 0) {
             float bx[5];
@@ -1197,7 +1214,7 @@ __global__ void roi_pool_bwd_kernel(const float* __restrict__ grad,
     }
     if (!IN_LDS) __builtin_amdgcn_s_waitcnt(0);
     const int nr = cnt[b];
-    const int* lst = list + static_cast<size_t>(b) * R;
+    const int* lst = list + static_cast<size_t>(b) * list_stride(R);
     for (int t = 0; t < nr; ++t) {
         const int n = __builtin_amdgcn_readfirstlane(lst[t]);
         const size_t base = (static_cast<size_t>(n) * C + c) * PHW;
@@ -1281,7 +1298,7 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_pf_kernel(
     const int n_ul = (has_u && has_l) ? lane - PW - 1 : lane;
     const int n_ur = (has_u && has_r) ? lane - PW + 1 : lane;
     if (nr > 0) {
-        const int* lst = list + static_cast<size_t>(b) * R;  // wave-uniform: scalar loads
+        const int* lst = list + static_cast<size_t>(b) * list_stride(R);  // wave-uniform: scalar loads
         const bool act = lane < PHW;
         // Loads are unconditional (idle lanes re-read bin 0, RoIs past the end
         // re-read the last one): a conditional load makes the compiler wait
@@ -1451,7 +1468,7 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
     const bool has_ul = has_u && has_l, has_ur = has_u && has_r;
     const bool has_dl = has_d && has_l, has_dr = has_d && has_r;
     if (nr > 0) {
-        const int* lst = list + static_cast<size_t>(b) * R;  // wave-uniform: scalar loads
+        const int* lst = list + static_cast<size_t>(b) * list_stride(R);  // wave-uniform: scalar loads
         const bool act = lane < PHW;
         const uint32_t kl = act ? lane : 0;
         // the host guarantees R*C*PHW*4 < 2^31: byte offsets fit the descriptors
@@ -1459,26 +1476,30 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
         const uint32_t mb = static_cast<uint32_t>(R) * PHW;
         const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(grad), 0, gb, 0x00020000);
         const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(argmax), 0, gb, 0x00020000);
+        // overlap masks are read only for flagged RoIs: the others load through
+        // a descriptor with no records (the load returns 0, no memory access)
         const auto rs_m = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(cmask), 0, mb * 8, 0x00020000);
-        const auto rs_c = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(code), 0, mb, 0x00020000);
+        const auto rs_0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(cmask), 0, 0, 0x00020000);
         const uint32_t cpb = static_cast<uint32_t>(c) * PHW * 4;
         const uint32_t rpb = static_cast<uint32_t>(C) * PHW * 4;
-        int am_r[D];
+        int am_r[D], fl_r[D];
         float g_r[D];
-        uint32_t cd_r[D], cl_r[D], ch_r[D];
-        // list positions past the image's RoIs re-read its last RoI (scalar
-        // clamp): the workspace tail is never written, and a raw buffer load's
-        // soffset is not range-checked, so a stale entry could address far
-        // past the buffers; those slots are dead (argmax -1)
+        uint32_t cl_r[D], ch_r[D];
+        // list entries: RoI index | flag << 31 (roi_lists_kernel with the codes);
+        // the flag drops out of the byte offsets (index x an even stride, mod
+        // 2^32).  Positions past the image's RoIs hold copies of its last entry
+        // (kListPad of them: a raw buffer load's soffset is not range-checked,
+        // so they must be real RoIs); those slots are dead (argmax -1).
+        static_assert(2 * D <= kListPad, "ring refills read up to 2D entries past the count");
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            const int n = lst[d < nr ? d : nr - 1];
-            const uint32_t so = static_cast<uint32_t>(n) * rpb + cpb;
-            const uint32_t sm = static_cast<uint32_t>(n) * PHW;
+            const int e = lst[d];
+            fl_r[d] = e < 0;
+            const uint32_t so = static_cast<uint32_t>(e) * rpb + cpb;
+            const uint32_t sm8 = static_cast<uint32_t>(e) * (PHW * 8);
             am_r[d] = __builtin_amdgcn_raw_buffer_load_b32(rs_a, kl * 4, so, 0);
             g_r[d] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g, kl * 4, so, 0));
-            cd_r[d] = __builtin_amdgcn_raw_buffer_load_b8(rs_c, kl, sm, 0);
-            const auto m = __builtin_amdgcn_raw_buffer_load_b64(rs_m, kl * 8, sm * 8, 0);
+            const auto m = __builtin_amdgcn_raw_buffer_load_b64(e < 0 ? rs_m : rs_0, kl * 8, sm8, 0);
             cl_r[d] = m[0];
             ch_r[d] = m[1];
             asm volatile("" ::: "memory");
@@ -1488,29 +1509,22 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
             const unsigned long long p0 = BPROF_T();
             int nx[D];
 #pragma unroll
-            for (int d = 0; d < D; ++d) {
-                const int tn = t0 + D + d;
-                nx[d] = lst[tn < nr ? tn : nr - 1];
-            }
+            for (int d = 0; d < D; ++d) nx[d] = lst[t0 + D + d];
             int am[D], addr[D];
             float g[D], s1[D], s3[D], s4[D];
             bool slow[D];
             // take the slot's argmax / grad / flag, then refill it with RoI t + D
 #pragma unroll
             for (int d = 0; d < D; ++d) {
-                uint32_t cd;
                 asm volatile("v_mov_b32 %0, %1" : "=v"(am[d]) : "v"(am_r[d]));
                 asm volatile("v_mov_b32 %0, %1" : "=v"(g[d]) : "v"(g_r[d]));
-                asm volatile("v_mov_b32 %0, %1" : "=v"(cd) : "v"(cd_r[d]));
                 const bool live = t0 + d < nr;
-                slow[d] = live && (__builtin_amdgcn_readfirstlane(cd) & 16) != 0;  // bin 0's code: the RoI flag
+                slow[d] = live && fl_r[d];
                 am[d] = live ? am[d] : -1;
                 am[d] = act ? am[d] : -2;
-                const int n = nx[d];
-                const uint32_t so = static_cast<uint32_t>(n) * rpb + cpb;
+                const uint32_t so = static_cast<uint32_t>(nx[d]) * rpb + cpb;
                 am_r[d] = __builtin_amdgcn_raw_buffer_load_b32(rs_a, kl * 4, so, 0);
                 g_r[d] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g, kl * 4, so, 0));
-                cd_r[d] = __builtin_amdgcn_raw_buffer_load_b8(rs_c, kl, static_cast<uint32_t>(n) * PHW, 0);
             }
             const unsigned long long p1 = BPROF_T();
             // neighbour exchanges, two slots per LDS round trip (each slot its
@@ -1568,9 +1582,8 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
                     const bool fol = static_cast<int>(has_l & (lo(q[e][0]) == a)) | (has_u & (lo(q[e][1]) == a)) |
                                      (has_ul & (lo(q[e][2]) == a)) | (has_ur & (lo(q[e][3]) == a));
                     // right and down-left never both match (they do not overlap)
-                    s1[d] = (has_r & (lo(q[e][4]) == a))    ? hi(q[e][4])
-                            : (has_dl & (lo(q[e][5]) == a)) ? hi(q[e][5])
-                                                            : -0.0f;
+                    const float t5 = (has_dl & (lo(q[e][5]) == a)) ? hi(q[e][5]) : -0.0f;
+                    s1[d] = (has_r & (lo(q[e][4]) == a)) ? hi(q[e][4]) : t5;
                     s3[d] = (has_d & (lo(q[e][6]) == a)) ? hi(q[e][6]) : -0.0f;
                     s4[d] = (has_dr & (lo(q[e][7]) == a)) ? hi(q[e][7]) : -0.0f;
                     addr[d] = (a >= 0 && !fol) ? a : HW + lane;
@@ -1588,10 +1601,11 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
                         }
                         addr[d] = depth;
                     }
-                    const uint32_t sm = static_cast<uint32_t>(nx[d]) * PHW;
-                    const auto m = __builtin_amdgcn_raw_buffer_load_b64(rs_m, kl * 8, sm * 8, 0);
+                    const uint32_t sm8 = static_cast<uint32_t>(nx[d]) * (PHW * 8);
+                    const auto m = __builtin_amdgcn_raw_buffer_load_b64(nx[d] < 0 ? rs_m : rs_0, kl * 8, sm8, 0);
                     cl_r[d] = m[0];
                     ch_r[d] = m[1];
+                    fl_r[d] = nx[d] < 0;
                 }
             }
             const unsigned long long p2 = BPROF_T();
@@ -1694,8 +1708,7 @@ struct FwdWs {
 FwdWs carve_fwd(void* ws, int64_t R, int N) {
     Carver c(ws);
     FwdWs w{};
-    // + 64: slack (kernels clamp list reads to each image's count)
-    w.list = c.take<int>(static_cast<size_t>(N + 1) * R + 64);
+    w.list = c.take<int>(static_cast<size_t>(N + 1) * list_stride(R));
     w.cnt = c.take<int>(N + 1);
     w.bytes = c.used();
     return w;
@@ -1783,7 +1796,12 @@ PxPlan pair_plan(int C, int N, int H, int W, int PHW, hipStream_t st) {
         pl.cg = cg;
         pl.lds = tile + static_cast<size_t>(pl.geo_cap) * kPerGeo;
         const int64_t wgs = static_cast<int64_t>(C / cg) * N;
-        int64_t sp = (static_cast<int64_t>(stream_cu_count(st)) * per_cu + wgs - 1) / wgs;
+        const int64_t slots = static_cast<int64_t>(stream_cu_count(st)) * per_cu;
+        // measured: the pair tiles win only with 8 channels per workgroup and
+        // one round of workgroups (cfg2); 4 channels (cfg4) or a second round
+        // (cfg5: 512 workgroups of one per CU) lose to the wave kernel
+        if (path_cfg().roi_fwd != kPathPair && (cg != 8 || wgs > slots)) return PxPlan{};
+        int64_t sp = (slots + wgs - 1) / wgs;
         if (path_cfg().roi_split > 0) sp = path_cfg().roi_split;  // A/B override
         pl.split = static_cast<int>(sp < 1 ? 1 : (sp > 64 ? 64 : sp));
         return pl;
@@ -1990,8 +2008,7 @@ BwdWs carve_bwd(void* ws, int64_t R, int N, int PH, int PW) {
     BwdWs w{};
     w.cmask = c.take<uint64_t>(static_cast<size_t>(R) * PH * PW);
     w.code = c.take<uint8_t>(static_cast<size_t>(R) * PH * PW);
-    // + 64: slack (kernels clamp list reads to each image's count)
-    w.list = c.take<int>(static_cast<size_t>(N + 1) * R + 64);
+    w.list = c.take<int>(static_cast<size_t>(N + 1) * list_stride(R));
     w.cnt = c.take<int>(N + 1);
     w.bytes = c.used();
     return w;
@@ -2035,18 +2052,19 @@ extern "C" int frcnn_roi_pool_bwd(const float* grad, const float* rois, const in
         hipLaunchKernelGGL(roi_bwd_prep_kernel, dim3(static_cast<unsigned>(R)), dim3(256), 0, st, rois,
                            H, W, PH, PW, spatial_scale, w.cmask, w.code);
     FRCNN_LAUNCH_CHECK("roi_bwd_prep_kernel");
-    hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, rois, static_cast<int>(R),
-                       N, w.list, w.cnt);
-    FRCNN_LAUNCH_CHECK("roi_lists_kernel");
     const size_t plane_bytes = HW * sizeof(float);
     const int PHW = PH * PW;
     const int bp = path_cfg().roi_bwd;
-    const bool ring = PHW <= 64 && bp != kPathPlain;
-    if (ring && plane_bytes <= kPlaneBudgetRing) {
-        // Every wave owns one (image, channel) plane and walks all of the
-        // image's RoIs, so the work per wave is fixed: spread the N*C waves
-        // evenly, one workgroup per CU (ceil(N*C / CUs) waves each) where the
-        // LDS allows -- a 2:1 mix of busy and half-idle CUs cost 1.35x.
+    const bool ring = PHW <= 64 && bp != kPathPlain && plane_bytes <= kPlaneBudgetRing;
+    // Every wave owns one (image, channel) plane and walks all of the image's
+    // RoIs, so the work per wave is fixed: spread the N*C waves evenly, one
+    // workgroup per CU (ceil(N*C / CUs) waves each) where the LDS allows -- a
+    // 2:1 mix of busy and half-idle CUs cost 1.35x.
+    int icpw = 1;
+    bool lead = false;
+    int HWs = 0;
+    size_t lead_bytes = 0;
+    if (ring) {
         const int64_t waves = static_cast<int64_t>(N) * C;
         int64_t cpw = (waves + device_cu_count() - 1) / device_cu_count();
         const int64_t lds_cap = static_cast<int64_t>(kPlaneBudgetRing / plane_bytes);
@@ -2054,12 +2072,19 @@ extern "C" int frcnn_roi_pool_bwd(const float* grad, const float* rois, const in
         cpw = cpw > lds_cap ? lds_cap : cpw;
         cpw = cpw > C ? C : cpw;
         cpw = cpw < 1 ? 1 : cpw;
-        const int icpw = static_cast<int>(cpw);
-        dim3 grid((C + icpw - 1) / icpw, N);
+        icpw = static_cast<int>(cpw);
         const bool fits = static_cast<uint64_t>(R) * C * PHW * 4 < (1ull << 31);
-        const int HWs = static_cast<int>((HW + 64 + 3) & ~static_cast<size_t>(3));  // + dummy words
-        const size_t lead_bytes = static_cast<size_t>(icpw) * (HWs * sizeof(float) + 2 * kBwdXRow * 8);
-        if (fits && bp == kPathAuto && PHW < 64 && PW == 7 && lead_bytes <= kPlaneBudgetRing)
+        HWs = static_cast<int>((HW + 64 + 3) & ~static_cast<size_t>(3));  // + dummy words
+        lead_bytes = static_cast<size_t>(icpw) * (HWs * sizeof(float) + 2 * kBwdXRow * 8);
+        lead = fits && bp == kPathAuto && PHW < 64 && PW == 7 && lead_bytes <= kPlaneBudgetRing;
+    }
+    // the leader kernel reads each RoI's path flag from its list entry
+    hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, rois, static_cast<int>(R), N, w.list,
+                       w.cnt, 5, lead ? w.code : nullptr, PHW);
+    FRCNN_LAUNCH_CHECK("roi_lists_kernel");
+    if (ring) {
+        dim3 grid((C + icpw - 1) / icpw, N);
+        if (lead)
             hipLaunchKernelGGL((roi_pool_bwd_lead_kernel<kBwdLead, 7>), grid, dim3(64 * icpw), lead_bytes,
                                st, grad, argmax, w.cmask, w.code, w.list, w.cnt, static_cast<int>(R), C,
                                static_cast<int>(HW), HWs, PHW, icpw, grad_in);

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--paths", default="hybrid,lazy,wide")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--cus", type=int, default=0, help="run on a stream masked to this many CUs (spread over XCDs)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     c = synth.CONFIGS[a.config]
@@ -35,6 +36,10 @@ def main():
                            post_nms=c["post_nms"], anchor_base=base, feat_h=c["feat_h"],
                            feat_w=c["feat_w"])
 
+    if a.cus > 0:
+        from bench import reserved_cus
+        torch.cuda.synchronize()
+        torch.cuda.set_stream(_lib.cu_stream(reserved_cus(_lib.cu_count(), a.cus, "rr")))
     paths = a.paths.split(",")
     times = {p: [] for p in paths}
     ref = None

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--variants", default="blocks,dense")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--exclude-cus", type=int, default=0,
+                    help="run on a stream masked to all CUs but this many (spread over XCDs)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     c = synth.CONFIGS[a.config]
@@ -44,6 +46,12 @@ def main():
     R = boxes.size(0)
     C, H, W = x.shape[1:]
     alg = N * C * H * W * 4 + R * 20 + 2 * R * C * 49 * 4
+    if a.exclude_cus > 0:
+        from bench import reserved_cus
+        n = _lib.cu_count()
+        res = set(reserved_cus(n, a.exclude_cus, "rr"))
+        torch.cuda.synchronize()
+        torch.cuda.set_stream(_lib.cu_stream([i for i in range(n) if i not in res]))
     variants = a.variants.split(",")
     ref = None
     times = {v: [] for v in variants}

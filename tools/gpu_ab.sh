@@ -8,5 +8,5 @@ for spec in "$@"; do
   cfg=${spec%%:*}; vars=${spec#*:}
   echo "[$(date +%T)] ab $cfg $vars"
   timeout -k 10 240 python -u tools/ab_roi_pool.py --config "$cfg" --variants "$vars" > "$OUT/ab_$cfg.json" 2>&1 || { tail -5 "$OUT/ab_$cfg.json"; exit 1; }
-  python3 -c "import json,sys; d=json.load(open('$OUT/ab_$cfg.json')); print('$cfg', {k: round(v['us_median'],1) for k,v in d['variants'].items()})"
+  python3 -c "import json; s=open('$OUT/ab_$cfg.json').read(); d=json.loads(s[s.index('{'):]); print('$cfg', {k: round(v['us_median'],1) for k,v in d['variants'].items()})"
 done
