@@ -483,6 +483,9 @@ def inference_step_fn(args, c, sets, base, world, n_total, backend, ev):
         ops.roi_pool_head(sets[0][2], prop_out[0][0].view(-1, 4), inds, 7, c["img_h"], c["img_w"],
                           rois_sorted=True, out=pool_outs[0])
     step.alone = alone
+    from replication_faster_rcnn_amd import _lib
+    step.kernel = _lib.roi_pool_fwd_kernel(N * post, N, C, x.size(2), x.size(3),
+                                           stream=s_props[0] if pool_on_prop else s_pool)
     return step
 
 
@@ -719,7 +722,7 @@ def main():
                    "devices": min(world, ndev)},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": DOMINANT_KERNEL["train" if train else "infer"],
+                     "kernel": DOMINANT_KERNEL["train"] if train else getattr(step, "kernel", DOMINANT_KERNEL["infer"]),
                      "basis": "pipeline-sustained: the dominant kernel's algorithmic bytes per step / "
                               "ms_per_step (one launch per step)",
                      "alg_bytes_per_launch": alg_bytes,

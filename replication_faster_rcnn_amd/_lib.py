@@ -43,6 +43,7 @@ SIGNATURES = {
     "frcnn_last_error": (ctypes.c_char_p, []),
     "frcnn_device_cu_count": (I32, [P]),
     "frcnn_set_path": (I32, [ctypes.c_char_p, ctypes.c_char_p]),
+    "frcnn_roi_pool_fwd_kernel": (I32, [I64, I32, I32, I32, I32, I32, I32, I32, I32, P, ctypes.c_char_p, SZ]),
     "frcnn_stream_create": (I32, [P, I32, P]),
     "frcnn_stream_destroy": (I32, [P]),
     "frcnn_stream_cu_count": (I32, [P, P]),
@@ -206,6 +207,18 @@ def stream_cu_count(stream) -> int:
     check(lib.frcnn_stream_cu_count(ctypes.c_void_p(stream.cuda_stream), ctypes.byref(n)),
           "stream_cu_count")
     return int(n.value)
+
+
+def roi_pool_fwd_kernel(R, N, C, H, W, PH=7, PW=7, rois_sorted=True, head=True, stream=None) -> str:
+    """frcnn_roi_pool_fwd_kernel: the template name of the RoIPool forward kernel
+    a call of this shape launches on `stream` (default: the current stream)."""
+    lib = load()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    buf = ctypes.create_string_buffer(128)
+    check(lib.frcnn_roi_pool_fwd_kernel(int(R), int(N), int(C), int(H), int(W), int(PH), int(PW),
+                                        int(bool(rois_sorted)), int(bool(head)),
+                                        ctypes.c_void_p(s.cuda_stream), buf, 128), "roi_pool_fwd_kernel")
+    return buf.value.decode()
 
 
 def set_path(op: str, path) -> None:

@@ -81,6 +81,12 @@ struct Carver {
 // ------------------------------------------------------------ device helpers
 constexpr int kWave = 64;
 
+// Latency-critical kernels (the proposal chain, the target creators and
+// samplers) raise their waves' issue priority: beside a VALU-bound kernel of
+// another step (the RoIPool) on the same SIMDs they would otherwise get a
+// fifth of the issue slots and stretch the step's critical path.
+__device__ __forceinline__ void latency_prio() { __builtin_amdgcn_s_setprio(3); }
+
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {

@@ -29,6 +29,7 @@
 #define FRCNN_POOL_EXP 0  // A/B probes: 1 = no output stores, 2 = no window scan
 #endif
 
+
 namespace frcnn {
 
 constexpr int kMaxBins = 1024;
@@ -814,12 +815,17 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
         for (int i = 1; i <= N; ++i) st[i] += st[i - 1];
     }
     __syncthreads();
+    PPROF_T(1);
     const int CGN = C / CG;
     const int64_t lo_v = st[0];
     const int64_t T = static_cast<int64_t>(CGN) * (st[N] - lo_v);
     const int G = static_cast<int>(gridDim.x) - 1;
-    int64_t u = T * static_cast<int64_t>(blockIdx.x) / G;
-    const int64_t u1 = T * (static_cast<int64_t>(blockIdx.x) + 1) / G;
+    // workgroup ids round-robin over the 8 XCDs: consecutive ranges (which share
+    // an image tile) go to one XCD, so the second staging of a tile hits its L2
+    const int xcd = blockIdx.x & 7, q8 = G >> 3, r8 = G & 7;
+    const int g = xcd * q8 + min(xcd, r8) + (static_cast<int>(blockIdx.x) >> 3);
+    int64_t u = T * static_cast<int64_t>(g) / G;
+    const int64_t u1 = T * (static_cast<int64_t>(g) + 1) / G;
     int b = 0;
     while (u < u1) {
         while (static_cast<int64_t>(CGN) * (st[b + 1] - lo_v) <= u) ++b;  // uniform (LDS, broadcast)
@@ -2352,6 +2358,41 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
                            st, x, rois, N, C, H, W, PH, PW, spatial_scale, out, argmax);
     FRCNN_LAUNCH_CHECK("roi_pool_fwd_kernel");
     return FRCNN_OK;
+}
+
+extern "C" int frcnn_roi_pool_fwd_kernel(int64_t R, int N, int C, int H, int W, int PH, int PW, int rois_sorted,
+                                         int head, void* stream, char* name, size_t len) {
+    FRCNN_REQUIRE(name && len > 0, "frcnn_roi_pool_fwd_kernel: null name");
+    FRCNN_REQUIRE(R >= 0 && N >= 0 && C >= 0 && H >= 0 && W >= 0 && PH > 0 && PW > 0,
+                  "frcnn_roi_pool_fwd_kernel: bad shape");
+    hipStream_t st = as_stream(stream);
+    const int path = path_cfg().roi_fwd;
+    const bool fix7 = PH == 7 && PW == 7;
+    const int fx = fix7 ? 7 : 0;
+    const char* hb = head ? "true" : "false";
+    const bool ok = rois_sorted && C > 0;
+    int n = 0;
+    const PxPlan rp = (ok && path == kPathRow) ? row_plan(C, N, H, W, PH, PW, st) : PxPlan{};
+    const PxPlan pp = (!rp.cg && ok && (path == kPathAuto || path == kPathPair)) ? pair_plan(C, N, H, W, PH * PW, st)
+                                                                                : PxPlan{};
+    const PxPlan xp = (!rp.cg && !pp.cg && ok && (path == kPathAuto || path == kPathWave || path == kPathPair))
+                          ? px_plan(C, N, H, W, PH * PW, st)
+                          : PxPlan{};
+    const DensePlan dp = (!rp.cg && !pp.cg && !xp.cg && path != kPathGeneric) ? dense_plan(C, N, H, W, PH * PW)
+                                                                              : DensePlan{};
+    if (rp.cg)
+        n = snprintf(name, len, "roi_pool_fwd_row_kernel<1024, %s>", hb);
+    else if (pp.cg)
+        n = snprintf(name, len, "roi_pool_fwd_pair_kernel<1024, %d, %d, %s>", pp.cg, fx, hb);
+    else if (xp.cg)
+        n = snprintf(name, len, "roi_pool_fwd_wave_kernel<1024, %d, %d, %s, %s>", xp.cg, fx, hb,
+                     xp.groups ? "true" : "false");
+    else if (dp.cg)
+        n = snprintf(name, len, "roi_pool_fwd_dense_kernel<1024, %d, %d, %s, %s>", dp.cg, fx,
+                     (head && rois_sorted) ? "true" : "false", rois_sorted ? "false" : "true");
+    else
+        n = snprintf(name, len, "roi_pool_fwd_kernel<%s>", (static_cast<size_t>(C) * PH * PW) % 4 == 0 ? "true" : "false");
+    return n < 0 ? FRCNN_EINVAL : FRCNN_OK;
 }
 
 extern "C" int frcnn_roi_pool_fwd_head(const float* x, const float* rois, const float* roi_inds,
