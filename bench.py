@@ -93,9 +93,6 @@ def parse():
     ap.add_argument("--roi-split", default="auto",
                     help="RoI shares per (image, channel group) of the RoIPool forward "
                          "(frcnn_set_path roi_pool_split): auto | 1 | 2 | ...")
-    ap.add_argument("--pool-free-cus", default="0",
-                    help="CUs the RoIPool forward grid leaves free for the next steps' proposal kernels "
-                         "(frcnn_set_path roi_pool_free_cus; balanced wave-kernel grid): 0 = fill every CU")
     ap.add_argument("--input-sets", type=int, default=0,
                     help="distinct input sets the steps cycle through (0 = enough for > 320 MiB, "
                          "i.e. more than the Infinity Cache; 1 = the same inputs every step)")
@@ -599,7 +596,7 @@ def main():
     from replication_faster_rcnn_amd import _lib
     from replication_faster_rcnn_amd import anchors as A
     for op, v in (("roi_pool_cg", args.roi_cg), ("roi_pool_split", args.roi_split),
-                  ("propose", args.propose_path), ("roi_pool_free_cus", args.pool_free_cus)):
+                  ("propose", args.propose_path)):
         if v != "auto":
             _lib.set_path(op, v)
     from replication_faster_rcnn_amd import dist as fdist
@@ -713,7 +710,6 @@ def main():
                    "prop_streams": args.prop_streams if (args.streams == 2 and not train) else 1,
                    "pool_on": args.pool_on if (args.streams == 2 and not train) else None,
                    "host_io": bool(args.host_io), "roi_cg": args.roi_cg, "roi_split": args.roi_split,
-                   "pool_free_cus": args.pool_free_cus,
                    "prop_cus": args.prop_cus if (args.streams == 2 and not train) else 0,
                    "propose_path": args.propose_path,
                    "collective": (None if world == 1 else

@@ -67,12 +67,10 @@ extern "C" int frcnn_set_path(const char* op, const char* path) {
     auto is = [&](const char* a, const char* b) { return std::strcmp(a, b) == 0; };
     const bool aut = is(path, "auto");
     if (is(op, "roi_pool_fwd") &&
-        (aut || is(path, "row") || is(path, "pair") || is(path, "wave") || is(path, "dense") ||
-         is(path, "generic"))) {
+        (aut || is(path, "pair") || is(path, "wave") || is(path, "dense") || is(path, "generic"))) {
         g_path.roi_fwd = aut ? kPathAuto : is(path, "generic") ? kPathGeneric
                                        : is(path, "dense")     ? kPathDense
                                        : is(path, "pair")      ? kPathPair
-                                       : is(path, "row")       ? kPathRow
                                                                : kPathWave;
     } else if (is(op, "roi_pool_bwd") &&
                (aut || is(path, "ring") || is(path, "plain"))) {
@@ -90,14 +88,6 @@ extern "C" int frcnn_set_path(const char* op, const char* path) {
             return FRCNN_EINVAL;
         }
         g_path.roi_split = static_cast<int>(v);
-    } else if (is(op, "roi_pool_free_cus")) {
-        char* end = nullptr;
-        const long v = aut ? 0 : std::strtol(path, &end, 10);
-        if (!aut && (end == path || *end != '\0' || v < 0 || v > 128)) {
-            set_error("frcnn_set_path: roi_pool_free_cus must be auto or 0..128, got '%s'", path);
-            return FRCNN_EINVAL;
-        }
-        g_path.roi_free_cus = static_cast<int>(v);
     } else if (is(op, "roi_pool_cg") && (aut || is(path, "4") || is(path, "8") || is(path, "16"))) {
         g_path.roi_cg = aut ? 0 : std::atoi(path);
     } else {

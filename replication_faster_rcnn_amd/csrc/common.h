@@ -20,7 +20,6 @@ constexpr int kPathGeneric = 1;  // roi_pool_fwd: one workgroup per RoI
 constexpr int kPathDense = 2;    // roi_pool_fwd: image tile, RoI bins packed per wave
 constexpr int kPathWave = 3;     // roi_pool_fwd: image tile, one wave per RoI (RoIs grouped by image)
 constexpr int kPathPair = 4;     // roi_pool_fwd: raw + pixel-pair tiles, one wave per RoI (grouped by image)
-constexpr int kPathRow = 5;      // roi_pool_fwd: pixel-major tile, one wave per RoI walking bin rows (7x7)
 constexpr int kPathPlain = 1;    // roi_pool_bwd: the unpipelined plane-owner kernel
 constexpr int kPathRing = 2;     // roi_pool_bwd: the RoI-at-a-time ring kernel (auto: leader kernel)
 constexpr int kPathHybrid = 1;   // propose: fused per image + chip-wide first-chunk mask
@@ -32,7 +31,6 @@ struct PathCfg {
     int propose = kPathAuto;
     int roi_split = 0;  // RoI shares per (image, channel group); 0 = auto
     int roi_cg = 0;     // channels per RoIPool workgroup (4 / 8 / 16); 0 = auto
-    int roi_free_cus = 0;  // RoIPool fwd (wave kernel): CUs its grid leaves free; 0 = fill every CU
 };
 const PathCfg& path_cfg();
 
@@ -80,12 +78,6 @@ struct Carver {
 
 // ------------------------------------------------------------ device helpers
 constexpr int kWave = 64;
-
-// Latency-critical kernels (the proposal chain, the target creators and
-// samplers) raise their waves' issue priority: beside a VALU-bound kernel of
-// another step (the RoIPool) on the same SIMDs they would otherwise get a
-// fifth of the issue slots and stretch the step's critical path.
-__device__ __forceinline__ void latency_prio() { __builtin_amdgcn_s_setprio(3); }
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 

@@ -93,7 +93,6 @@ __global__ __launch_bounds__(256) void decode_filter_kernel(
     const float4* __restrict__ anchors, const float4* __restrict__ base, int A, int K, int W,
     int stride, float img_h, float img_w, float min_size, float4* __restrict__ boxes,
     uint64_t* __restrict__ keys) {
-    latency_prio();
     int a = blockIdx.x * 256 + threadIdx.x;
     if (a >= A) return;
     size_t o = static_cast<size_t>(blockIdx.y) * A + a;
@@ -122,7 +121,6 @@ __global__ __launch_bounds__(256) void decode_filter_kernel(
 // keys for the plain nms op: every box valid, index order breaks ties.
 __global__ __launch_bounds__(256) void nms_keys_kernel(const float* __restrict__ scores, int n,
                                                        uint64_t* __restrict__ keys) {
-    latency_prio();
     int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     keys[i] = (static_cast<uint64_t>(desc_score_key(scores[i])) << 32) | static_cast<uint32_t>(i);
@@ -159,7 +157,6 @@ __device__ __forceinline__ int lower_bound_u64(const uint64_t* s, int len, uint6
 
 __global__ __launch_bounds__(1024) void run_sort_kernel(const uint64_t* __restrict__ keys_all, int A, int nr,
                                                         uint64_t* __restrict__ runs_all, int* __restrict__ vcount) {
-    latency_prio();
     const int n = blockIdx.y, i = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int base = i * kRun;
@@ -200,7 +197,6 @@ __global__ __launch_bounds__(1024) void run_sort_kernel(const uint64_t* __restri
 // Workgroup (i, j): for every key of run i, the number of keys of run j below it.
 __global__ __launch_bounds__(1024) void merge_rank_kernel(const uint64_t* __restrict__ runs_all, int A, int nr,
                                                           int* __restrict__ part) {
-    latency_prio();
     const int n = blockIdx.z, j = blockIdx.y, i = blockIdx.x;
     if (i == j) return;
     const int tid = threadIdx.x;
@@ -229,7 +225,6 @@ __global__ __launch_bounds__(1024) void rank_scatter_kernel(const uint64_t* __re
                                                             int pre, const float4* __restrict__ box_src,
                                                             float4* __restrict__ sbox, int32_t* __restrict__ sidx,
                                                             int* __restrict__ sel_P, SweepState ss) {
-    latency_prio();
     const int n = blockIdx.y, i = blockIdx.x;
     const int tid = threadIdx.x;
     int nvalid = 0;
@@ -303,7 +298,6 @@ __global__ __launch_bounds__(256) void nms_mask_stage_kernel(const float4* __res
                                                              uint64_t* __restrict__ maskC,
                                                              const uint64_t* __restrict__ kept_all,
                                                              uint64_t* __restrict__ prehit) {
-    latency_prio();
     const int n = blockIdx.y;
     if (done[n]) return;
     const int P = sel_P[n];
@@ -382,7 +376,6 @@ __global__ __launch_bounds__(1024) void nms_sweep_stage_kernel(
     const int32_t* __restrict__ sidx_all, int pre, int Wc, const int* __restrict__ sel_P, int post,
     int cb0, int cb1, SweepState ss, float4* __restrict__ out_rois, int32_t* __restrict__ out_idx,
     int64_t* __restrict__ out_keep, int32_t* __restrict__ out_count) {
-    latency_prio();
     extern __shared__ __attribute__((aligned(16))) uint64_t kept[];  // [Wc]
     __shared__ uint64_t s_K[2];
     __shared__ int s_count[2];
@@ -599,7 +592,6 @@ constexpr int kChunkTiles = kChunkBlocks * (kChunkBlocks + 1) / 2;  // 136
 __global__ __launch_bounds__(256) void chunk_colmask_kernel(const float4* __restrict__ cbox_all,
                                                             const int* __restrict__ cc_all, NmsThr thr,
                                                             uint64_t* __restrict__ colT) {
-    latency_prio();
     const int n = blockIdx.y;
     const int cc = cc_all[n];
     const int nb = (cc + 63) / 64;
@@ -718,7 +710,6 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
     const uint64_t* __restrict__ keys_all, const float4* __restrict__ boxes_all, int A, int pre,
     int post, NmsThr thr, float4* __restrict__ out_rois, int32_t* __restrict__ out_idx,
     int32_t* __restrict__ out_count, HybWs hw) {
-    latency_prio();
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     __shared__ FusedShared sh;
     unsigned* hist = reinterpret_cast<unsigned*>(lds_raw);                          // 16 KB

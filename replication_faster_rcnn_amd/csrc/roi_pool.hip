@@ -25,11 +25,6 @@
 
 #include "common.h"
 
-#ifndef FRCNN_POOL_EXP
-#define FRCNN_POOL_EXP 0  // A/B probes: 1 = no output stores, 2 = no window scan
-#endif
-
-
 namespace frcnn {
 
 constexpr int kMaxBins = 1024;
@@ -557,7 +552,6 @@ __device__ unsigned int g_pool_prof_rois[kPoolProfSlots];
 #define PPROF_ROIS(n) do {} while (0)
 #endif
 
-
 // Tile layout of the wave-per-RoI forward: 16-pixel groups, the group's NP
 // 4-channel planes back to back (pixel p of plane q at float4
 // (g*NP + q)*16 + s, g = p >> 4), the slot s = (p ^ g) & 15 XOR-swizzled so
@@ -591,21 +585,55 @@ __device__ __forceinline__ const float4* tile_px(const float4* q4, int p) {
 // shape per image or per RoI block -- are slower: DESIGN.md §3.)
 // FIX = PH = PW known at compile time (the 7x7 head): the 2 x CG output
 // stores of a RoI take immediate offsets from one base address.
-// One (image b, channel group c0) segment of the wave-per-RoI forward: stage
-// the group's planes (tile_px layout), then pool the RoIs r_base +
-// (r_a + k * r_d) mod r_n, k < nmine, one wave per RoI pulled from an LDS
-// counter.  Ends with a barrier (the tile and the geometry chunk may be reused
-// at once).
 template <int NT, int CG, int FIX, bool HEAD>
-__device__ __forceinline__ void wave_seg(const float* __restrict__ x, const float* __restrict__ rois, int C, int H,
-                                         int W, int PH, int PW, float ss, float* __restrict__ out,
-                                         int32_t* __restrict__ argmax, int geo_cap, const HeadArgs& hd, int b, int c0,
-                                         int r_base, int r_a, int r_d, int r_n, int nmine, float4* q4, int& s_next) {
+__global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
+    const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W, int PH_, int PW_,
+    float ss, float* __restrict__ out, int32_t* __restrict__ argmax, int geo_cap, HeadArgs hd) {
+    const int PH = FIX ? FIX : PH_, PW = FIX ? FIX : PW_;
     constexpr int NP = CG / 4;
+    extern __shared__ __attribute__((aligned(16))) float4 q4[];  // plane k at q4 + k * HWs; geometry after
+    __shared__ int s_red[2 * (NT / 64)];
+    __shared__ int s_next;
+    const int b = blockIdx.z;
+    const int c0 = blockIdx.x * CG;
     const int tid = threadIdx.x, lane = tid & 63;
     const int HW = H * W;
     const int HWs = (HW + 16) & ~15;  // + the zero sentinel pixel HW
     const int PHW = PH * PW;
+    const int split = gridDim.y, z = blockIdx.y;
+    const int N = gridDim.z - 1;
+    PPROF_T(0);
+    if (b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
+        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, 0, N, s_red, 1)
+                             : roi_range_sorted<NT>(rois, R, 0, N, s_red);
+        const int n_lo = rg.x, tot = n_lo + (R - rg.y);
+        const int lo = static_cast<int>(static_cast<int64_t>(tot) * z / split);
+        const int hi = static_cast<int>(static_cast<int64_t>(tot) * (z + 1) / split);
+        if (HEAD && hd.boxes && blockIdx.x == 0)
+            for (int t = lo + tid; t < hi; t += NT) {
+                const int r = t < n_lo ? t : rg.y + (t - n_lo);
+                float bx[5];
+                head_box(rois, hd, r, bx);
+#pragma unroll
+                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
+            }
+        for (int e = lo * CG * PHW + tid; e < hi * CG * PHW; e += NT) {
+            const int t = e / (CG * PHW);
+            const int rem = e - t * (CG * PHW);
+            const int r = t < n_lo ? t : rg.y + (t - n_lo);
+            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + rem;
+            out[o] = 0.0f;
+            argmax[o] = -1;
+        }
+        return;
+    }
+    const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, b, b + 1, s_red, 1)
+                         : roi_range_sorted<NT>(rois, R, b, b + 1, s_red);
+    const int rbase = rg.x, nr = rg.y - rg.x;
+    PPROF_T(1);
+    if (z >= nr) return;
+    const int nmine = (nr - z + split - 1) / split;  // items z, z+split, ...
+    PPROF_ROIS(nmine);
     const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
     if (tid < NP) const_cast<float4*>(tile_px<NP>(q4, HW))[16 * tid] = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int p = tid; p < HW; p += NT) {
@@ -626,11 +654,11 @@ __device__ __forceinline__ void wave_seg(const float* __restrict__ x, const floa
     for (int k0 = 0; k0 < nmine; k0 += geo_cap) {
         const int cn = min(geo_cap, nmine - k0);
         for (int i = tid; i < cn; i += NT) {
-            const int r = r_base + static_cast<int>((r_a + static_cast<int64_t>(k0 + i) * r_d) % r_n);
+            const int r = rbase + z + (k0 + i) * split;
             float bx[5];
             if (HEAD) {
                 head_box(rois, hd, r, bx);
-                if (hd.boxes && c0 == 0) {
+                if (hd.boxes && blockIdx.x == 0) {
 #pragma unroll
                     for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
                 }
@@ -650,7 +678,7 @@ __device__ __forceinline__ void wave_seg(const float* __restrict__ x, const floa
         while (k < cn) {
             int kn = 0;
             if (lane == 0) kn = atomicAdd(&s_next, 1);  // prefetch the next item
-            const int r = r_base + static_cast<int>((r_a + static_cast<int64_t>(k0 + k) * r_d) % r_n);
+            const int r = rbase + z + (k0 + k) * split;
             const int4 gq = s_geo[k];
             RoiGeom gm;
             gm.sh = gq.x;
@@ -683,7 +711,7 @@ __device__ __forceinline__ void wave_seg(const float* __restrict__ x, const floa
                     }
                 }
             }
-            for (int h = g.x; h < (FRCNN_POOL_EXP == 2 ? g.x : g.y); ++h) {
+            for (int h = g.x; h < g.y; ++h) {
                 const int rb = h * W;
                 for (int w = h == g.x ? g.z + 1 : g.z; w < g.w; ++w) {
                     const int ii = rb + w;
@@ -707,11 +735,7 @@ __device__ __forceinline__ void wave_seg(const float* __restrict__ x, const floa
                     }
                 }
             }
-#if FRCNN_POOL_EXP == 1
-            if (act && mv[0] == 1.2345e-30f) {
-#else
             if (act) {
-#endif
                 const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
                 float* op = out + o;
                 int32_t* ap = argmax + o;
@@ -724,133 +748,6 @@ __device__ __forceinline__ void wave_seg(const float* __restrict__ x, const floa
             k = __builtin_amdgcn_readfirstlane(kn);
         }
         __syncthreads();  // the chunk's geometry and s_next are reused
-    }
-}
-
-// Grid (C/CG, split, N + 1); BAL ("balanced", frcnn_set_path("roi_pool_free_cus", k)):
-// grid (G + 1) for G workgroups over the flattened (image, channel group, RoI)
-// units -- G = the launch stream's CUs minus k, so k CUs stay free for
-// concurrent kernels (the next step's proposal workgroups) instead of a
-// 2-per-image-group split rounding the grid up to every CU -- each workgroup
-// a contiguous range of about T / G units (one or two segments, a restaged tile
-// per segment); the last workgroup handles out-of-range batch indices.
-template <int NT, int CG, int FIX, bool HEAD, bool BAL>
-__global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
-    const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W, int PH_, int PW_,
-    float ss, float* __restrict__ out, int32_t* __restrict__ argmax, int geo_cap, HeadArgs hd, int NB) {
-    const int PH = FIX ? FIX : PH_, PW = FIX ? FIX : PW_;
-    constexpr int NP = CG / 4;
-    extern __shared__ __attribute__((aligned(16))) float4 q4[];  // plane k at q4 + k * HWs; geometry after
-    __shared__ int s_red[2 * (NT / 64)];
-    __shared__ int s_next;
-    const int tid = threadIdx.x;
-    const int HW = H * W;
-    const int HWs = (HW + 16) & ~15;
-    const int PHW = PH * PW;
-    const int N = BAL ? NB : static_cast<int>(gridDim.z) - 1;
-    const int split = BAL ? 1 : gridDim.y;
-    const int z = BAL ? 0 : blockIdx.y;
-    const bool inval = BAL ? blockIdx.x == gridDim.x - 1 : blockIdx.z == static_cast<unsigned>(N);
-    PPROF_T(0);
-    if (inval) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
-        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, 0, N, s_red, 1)
-                             : roi_range_sorted<NT>(rois, R, 0, N, s_red);
-        const int n_lo = rg.x, tot = n_lo + (R - rg.y);
-        const int lo = static_cast<int>(static_cast<int64_t>(tot) * z / split);
-        const int hi = static_cast<int>(static_cast<int64_t>(tot) * (z + 1) / split);
-        const int c_lo = BAL ? 0 : blockIdx.x * CG, c_n = BAL ? C : CG;
-        if (HEAD && hd.boxes && c_lo == 0)
-            for (int t = lo + tid; t < hi; t += NT) {
-                const int r = t < n_lo ? t : rg.y + (t - n_lo);
-                float bx[5];
-                head_box(rois, hd, r, bx);
-#pragma unroll
-                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
-            }
-        for (int64_t e = static_cast<int64_t>(lo) * c_n * PHW + tid; e < static_cast<int64_t>(hi) * c_n * PHW; e += NT) {
-            const int t = static_cast<int>(e / (c_n * PHW));
-            const int rem = static_cast<int>(e - static_cast<int64_t>(t) * (c_n * PHW));
-            const int r = t < n_lo ? t : rg.y + (t - n_lo);
-            const size_t o = (static_cast<size_t>(r) * C + c_lo) * PHW + rem;
-            out[o] = 0.0f;
-            argmax[o] = -1;
-        }
-        return;
-    }
-    if (!BAL) {
-        const int b = blockIdx.z;
-        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, b, b + 1, s_red, 1)
-                             : roi_range_sorted<NT>(rois, R, b, b + 1, s_red);
-        const int rbase = rg.x, nr = rg.y - rg.x;
-        PPROF_T(1);
-        if (z >= nr) return;
-        const int nmine = (nr - z + split - 1) / split;  // items z, z+split, ...
-        PPROF_ROIS(nmine);
-        wave_seg<NT, CG, FIX, HEAD>(x, rois, C, H, W, PH, PW, ss, out, argmax, geo_cap, hd, b, blockIdx.x * CG,
-                                    rbase, z, split, nr, nmine, q4, s_next);
-        PPROF_T(3);
-        return;
-    }
-    // ---- balanced: image starts (RoIs grouped by non-decreasing batch index)
-    // counted into LDS after the geometry chunk: st[b] = first RoI of image b,
-    // st[N] = end of the valid RoIs
-    int* st = reinterpret_cast<int*>(reinterpret_cast<int4*>(q4 + NP * HWs) + geo_cap);
-    for (int i = tid; i <= N; i += NT) st[i] = 0;
-    __syncthreads();
-    const float* bidx = HEAD ? hd.inds : rois;
-    const int bst = HEAD ? 1 : 5;
-    int n_lo = 0;
-    for (int r = tid; r < R; r += NT) {
-        const int rb = static_cast<int>(bidx[static_cast<size_t>(r) * bst]);
-        if (rb >= 0 && rb < N) atomicAdd(&st[rb + 1], 1);
-        n_lo += rb < 0;
-    }
-    n_lo = static_cast<int>(wave_sum_u32(static_cast<uint32_t>(n_lo)));
-    if ((tid & 63) == 0) s_red[tid >> 6] = n_lo;
-    __syncthreads();
-    if (tid == 0) {
-        int lo = 0;
-        for (int w = 0; w < NT / 64; ++w) lo += s_red[w];
-        st[0] = lo;
-        for (int i = 1; i <= N; ++i) st[i] += st[i - 1];
-    }
-    __syncthreads();
-    PPROF_T(1);
-    const int CGN = C / CG;
-    const int64_t lo_v = st[0];
-    const int64_t T = static_cast<int64_t>(CGN) * (st[N] - lo_v);
-    const int G = static_cast<int>(gridDim.x) - 1;
-    // workgroup ids round-robin over the 8 XCDs: consecutive ranges (which share
-    // an image tile) go to one XCD, so the second staging of a tile hits its L2
-    const int xcd = blockIdx.x & 7, q8 = G >> 3, r8 = G & 7;
-    const int g = xcd * q8 + min(xcd, r8) + (static_cast<int>(blockIdx.x) >> 3);
-    int64_t u = T * static_cast<int64_t>(g) / G;
-    const int64_t u1 = T * (static_cast<int64_t>(g) + 1) / G;
-    int b = 0;
-    while (u < u1) {
-        while (static_cast<int64_t>(CGN) * (st[b + 1] - lo_v) <= u) ++b;  // uniform (LDS, broadcast)
-        const int sb = st[b], nb = st[b + 1] - sb;
-        const int64_t rem = u - static_cast<int64_t>(CGN) * (sb - lo_v);
-        const int cg = static_cast<int>(rem / nb);
-        const int i0 = static_cast<int>(rem - static_cast<int64_t>(cg) * nb);
-        const int cnt = static_cast<int>(min(static_cast<int64_t>(nb - i0), u1 - u));
-        // unit i of the pair is RoI (i * sd) mod nb, sd coprime to nb near nb / golden
-        // ratio: any contiguous unit range samples the whole score order (RoI cost
-        // falls with NMS rank: a contiguous half of an image's RoIs costs ~20 % more)
-        int sd = static_cast<int>(0.6180340f * static_cast<float>(nb)) | 1;
-        for (;; sd += 2) {
-            int a = sd, c = nb;
-            while (c) {
-                const int t = a % c;
-                a = c;
-                c = t;
-            }
-            if (a == 1 || sd >= nb) break;
-        }
-        if (sd >= nb) sd = 1;
-        wave_seg<NT, CG, FIX, HEAD>(x, rois, C, H, W, PH, PW, ss, out, argmax, geo_cap, hd, b, cg * CG, sb,
-                                    static_cast<int>(static_cast<int64_t>(i0) * sd % nb), sd, nb, cnt, q4, s_next);
-        u += cnt;
     }
     PPROF_T(3);
 }
@@ -1024,11 +921,7 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_pair_kernel(
             const int r = rbase + z + (k0 + k) * split;
             const int4 gq = s_geo[k];
             const int ext = __builtin_amdgcn_readfirstlane(s_ext[k]);
-#if FRCNN_POOL_EXP == 2
-            const int Hm = 0, Um = ext & 0xffff;
-#else
             const int Hm = ext >> 16, Um = ext & 0xffff;
-#endif
             RoiGeom gm;
             gm.sh = gq.x;
             gm.sw = gq.y;
@@ -1078,11 +971,7 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_pair_kernel(
                 }
                 rowpix += W;
             }
-#if FRCNN_POOL_EXP == 1
-            if (act && m[0] == 1.2345e-30f) {
-#else
             if (act) {
-#endif
                 const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + bin;
                 float* op = out + o;
                 int32_t* ap = argmax + o;
@@ -1090,247 +979,6 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_pair_kernel(
                 for (int c = 0; c < CG; ++c) {
                     op[c * PHW] = m[c];
                     ap[c * PHW] = (X[c] >> 8) + ((X[c] >> c) & 1);
-                }
-            }
-            k = __builtin_amdgcn_readfirstlane(kn);
-        }
-        __syncthreads();  // the chunk's geometry and s_next are reused
-    }
-}
-
-// ------------------------------------------------- bin-row forward (7x7)
-// The default forward for the 7x7 head when an image's 16-channel tile fits
-// the CU's LDS.  Same grid and RoI shares as the wave kernel; the tile is
-// pixel-major, one pixel's 16 channels = 64 contiguous bytes.  One wave per
-// RoI; lane = (bin column pw = lane / 8, channel pair k = lane % 8), lanes
-// 56..63 idle.  The wave walks the RoI one BIN ROW at a time: the seven bins
-// of a row share their window rows (wave-uniform loop bounds), only their
-// columns differ (widths w or w + 1, clipped ones less).  A lane scans its
-// window as column PAIRS (ws + 2t, ws + 2t + 1), the last pair clamped to
-// (we - 2, we - 1) -- re-visited pixels never pass a strict '>' again -- and
-// 1-wide windows as (ws, ws):
-//     m' = max3(m, a, b);  if (m' > m) rec = pair address;  m = m'
-// (one full-rate max3 + compare + select per channel per TWO pixels, instead
-// of a compare and two selects per pixel).  After the row the recorded pair is
-// re-read: the first maximum in torchvision's row-major strict-'>' order is
-// its first pixel iff that equals the maximum (no earlier pair reached it),
-// and the output value is the re-read pixel itself (exact bits: the sign of a
-// zero maximum, never a max3-canonicalised value).  The tile holds NaN as
-// -inf: neither ever passes torchvision's '>' against -FLT_MAX.  The pair
-// address doubles as the argmax record (pixel = address / 64).
-// Stores: per bin row, 4 dword stores (out / argmax x 2 channels) of 7-bin
-// runs with immediate offsets.
-__host__ __device__ constexpr size_t row_tile_bytes(int HW) { return static_cast<size_t>(HW) * 64; }
-
-// One bin row of the bin-row forward: nstep pair steps, step s = pair
-// s % npair of window row s / npair; each pair at colb + row offset +
-// min(128 t, lastp); SEC64: every lane's second pixel 64 B on (immediate),
-// else `sec`.  Two steps per iteration with the next step's reads issued
-// before this step's update; an odd count repeats the last step (a repeated
-// pair never passes the strict '>').  Scalar bookkeeping only.
-// LDS loads at absolute LDS byte addresses (the row kernel's tile starts at
-// address 0): constant offsets fold into the instruction's offset field.
-typedef __attribute__((address_space(3))) const uint64_t lds_u64;
-typedef __attribute__((address_space(3))) const float lds_float;
-__device__ __forceinline__ float2 lds_ld2(int ad) {
-    const uint64_t v = *reinterpret_cast<lds_u64*>(static_cast<uintptr_t>(ad));
-    return make_float2(__uint_as_float(static_cast<uint32_t>(v)), __uint_as_float(static_cast<uint32_t>(v >> 32)));
-}
-__device__ __forceinline__ float lds_ld(int ad) { return *reinterpret_cast<lds_float*>(static_cast<uintptr_t>(ad)); }
-
-template <bool SEC64>
-__device__ __forceinline__ void row_scan(int colb, int lastp, int sec, int rowoff, int rowb,
-                                         int npair, int nstep, float& m0, float& m1, int& a0, int& a1) {
-    int t = 0;
-    auto at = [&](int ro, int tt) { return colb + ro + min(128 * tt, lastp); };
-    auto rd = [&](int ad) { return lds_ld2(ad); };
-    auto rd2 = [&](int ad) { return SEC64 ? lds_ld2(ad + 64) : lds_ld2(ad + sec); };
-    auto next = [&](int valid) {  // advance (rowoff, t) to the next step when valid
-        const int tn = t + 1 == npair ? 0 : t + 1;
-        const int rn = t + 1 == npair ? rowoff + rowb : rowoff;
-        t = valid ? tn : t;
-        rowoff = valid ? rn : rowoff;
-    };
-    auto upd = [&](int ad, float2 va, float2 vb) {
-        const float n0 = max3_raw(m0, va.x, vb.x);
-        const float n1 = max3_raw(m1, va.y, vb.y);
-        a0 = n0 > m0 ? ad : a0;
-        a1 = n1 > m1 ? ad : a1;
-        m0 = n0;
-        m1 = n1;
-    };
-    int adA = at(rowoff, t);
-    float2 aA = rd(adA), bA = rd2(adA);
-    for (int s = 0; s < nstep; s += 2) {
-        next(s + 1 < nstep);
-        const int adB = at(rowoff, t);
-        const float2 aB = rd(adB), bB = rd2(adB);
-        upd(adA, aA, bA);
-        next(s + 2 < nstep);
-        adA = at(rowoff, t);
-        aA = rd(adA);
-        bA = rd2(adA);
-        upd(adB, aB, bB);
-    }
-}
-
-template <int NT, bool HEAD>
-__global__ __launch_bounds__(NT) void roi_pool_fwd_row_kernel(
-    const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W, float ss,
-    float* __restrict__ out, int32_t* __restrict__ argmax, int geo_cap, HeadArgs hd) {
-    constexpr int CG = 16, P = 7, PHW = 49;
-    // dynamic LDS only (the tile starts at address 0, so tile offsets need no
-    // base add): tile | geometry chunk | s_red | s_next
-    extern __shared__ __attribute__((aligned(16))) float4 q4[];
-    int* s_red = reinterpret_cast<int*>(reinterpret_cast<int4*>(q4 + 4 * H * W) + geo_cap);
-    int& s_next = s_red[2 * (NT / 64)];
-    const int b = blockIdx.z;
-    const int c0 = blockIdx.x * CG;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int HW = H * W;
-    const int split = gridDim.y, z = blockIdx.y;
-    const int N = gridDim.z - 1;
-    if (b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
-        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, 0, N, s_red, 1)
-                             : roi_range_sorted<NT>(rois, R, 0, N, s_red);
-        const int n_lo = rg.x, tot = n_lo + (R - rg.y);
-        const int lo = static_cast<int>(static_cast<int64_t>(tot) * z / split);
-        const int hi = static_cast<int>(static_cast<int64_t>(tot) * (z + 1) / split);
-        if (HEAD && hd.boxes && blockIdx.x == 0)
-            for (int t = lo + tid; t < hi; t += NT) {
-                const int r = t < n_lo ? t : rg.y + (t - n_lo);
-                float bx[5];
-                head_box(rois, hd, r, bx);
-#pragma unroll
-                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
-            }
-        for (int e = lo * CG * PHW + tid; e < hi * CG * PHW; e += NT) {
-            const int t = e / (CG * PHW);
-            const int rem = e - t * (CG * PHW);
-            const int r = t < n_lo ? t : rg.y + (t - n_lo);
-            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + rem;
-            out[o] = 0.0f;
-            argmax[o] = -1;
-        }
-        return;
-    }
-    const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, b, b + 1, s_red, 1)
-                         : roi_range_sorted<NT>(rois, R, b, b + 1, s_red);
-    const int rbase = rg.x, nr = rg.y - rg.x;
-    if (z >= nr) return;
-    const int nmine = (nr - z + split - 1) / split;  // items z, z+split, ...
-    // ---- stage the tile: thread -> (pixel, 4-channel quad); NaN -> -inf
-    {
-        const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
-        const int q = tid & 3;
-        for (int p = tid >> 2; p < HW; p += NT / 4) {
-            float v[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float e = src[static_cast<size_t>(4 * q + j) * HW + p];
-                v[j] = e != e ? -INFINITY : e;
-            }
-            q4[4 * p + q] = make_float4(v[0], v[1], v[2], v[3]);
-        }
-    }
-    int4* s_geo = reinterpret_cast<int4*>(q4 + 4 * HW);
-    const int slot = lane >> 3, kp = lane & 7;
-    const bool act = slot < P;
-    const int rowb = W * 64;
-    for (int k0 = 0; k0 < nmine; k0 += geo_cap) {
-        const int cn = min(geo_cap, nmine - k0);
-        for (int i = tid; i < cn; i += NT) {
-            const int r = rbase + z + (k0 + i) * split;
-            float bx[5];
-            if (HEAD) {
-                head_box(rois, hd, r, bx);
-                if (hd.boxes && blockIdx.x == 0) {
-#pragma unroll
-                    for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 5; ++j) bx[j] = rois[static_cast<size_t>(r) * 5 + j];
-            }
-            const RoiGeom gm = roi_geom(bx, ss, P, P);
-            s_geo[i] = make_int4(gm.sh, gm.sw, __float_as_int(gm.bh), __float_as_int(gm.bw));
-        }
-        if (tid == 0) s_next = 0;
-        __syncthreads();  // tile staged (first chunk) / geometry of the chunk
-        int k = 0;
-        if (lane == 0) k = atomicAdd(&s_next, 1);
-        k = __builtin_amdgcn_readfirstlane(k);
-        while (k < cn) {
-            int kn = 0;
-            if (lane == 0) kn = atomicAdd(&s_next, 1);  // prefetch the next item
-            const int r = rbase + z + (k0 + k) * split;
-            const int4 gq = s_geo[k];
-            RoiGeom gm;
-            gm.sh = gq.x;
-            gm.sw = gq.y;
-            gm.bh = __int_as_float(gq.z);
-            gm.bw = __int_as_float(gq.w);
-            // lane slot s: the columns of bin column s and the rows of bin row s
-            const int4 g = geom_bin(gm, H, W, act ? slot : 0, act ? slot : 0);
-            const int ww = act ? g.w - g.z : 0;  // >= 0 (clamping keeps ws <= we)
-            int wmax = 0, wmin = 1 << 20;  // over the bins with a column range
-#pragma unroll
-            for (int q = 0; q < P; ++q) {
-                const int wq = __builtin_amdgcn_readlane(ww, 8 * q);
-                wmax = max(wmax, wq);
-                wmin = wq > 0 ? min(wmin, wq) : wmin;
-            }
-            // every pair is two distinct pixels (empty windows read (0, 1), unused):
-            // the second pixel at an immediate offset
-            const bool sec_uni = wmin >= 2;
-            // per lane: byte offset of its first column in a row, last pair start,
-            // offset of the pair's second pixel (0 for 1-wide / empty windows)
-            const int colb = (ww > 0 ? g.z * 64 : 0) + kp * 8;
-            const int lastp = ww >= 2 ? (ww - 2) * 64 : 0;
-            const int sec = (ww >= 2 || (sec_uni && ww == 0)) ? 64 : 0;
-            const int npair = (wmax + 1) >> 1;
-            const size_t ob = (static_cast<size_t>(r) * C + c0 + 2 * kp) * PHW + slot;
-            float* op = out + ob;
-            int32_t* ap = argmax + ob;
-#pragma unroll 1
-            for (int ph = 0; ph < P; ++ph) {
-                const int hs = __builtin_amdgcn_readlane(g.x, 8 * ph);
-                const int he = __builtin_amdgcn_readlane(g.y, 8 * ph);
-                float m0 = -FLT_MAX, m1 = -FLT_MAX;
-                int a0 = -1, a1 = -1;
-                const bool rows = he > hs && wmax > 0;
-                if (rows) {
-                    // (SEC64 lets the compiler merge the two pixel reads into one
-                    // ds_read2_b64, which moves half the bytes per LDS cycle of two
-                    // ds_read_b64: the per-lane offset is kept)
-                    row_scan<false>(colb, lastp, sec, hs * rowb, rowb, npair, (he - hs) * npair, m0, m1, a0, a1);
-                    // decode: the recorded pair's first pixel holds the first maximum
-                    // iff it equals the maximum; the output is the pixel's own value
-                    if (a0 >= 0) {
-                        const float pa = lds_ld(a0);
-                        const float pb = lds_ld(a0 + sec);
-                        const bool first = pa == m0;
-                        m0 = first ? pa : pb;
-                        a0 = (a0 >> 6) + (first ? 0 : 1);
-                    }
-                    if (a1 >= 0) {
-                        const float pa = lds_ld(a1 + 4);
-                        const float pb = lds_ld(a1 + 4 + sec);
-                        const bool first = pa == m1;
-                        m1 = first ? pa : pb;
-                        a1 = (a1 >> 6) + (first ? 0 : 1);
-                    }
-                }
-                const bool empty = !rows || ww == 0;
-#if FRCNN_POOL_EXP == 1
-                if (act && m0 == 1.2345e-30f) {
-#else
-                if (act) {
-#endif
-                    op[ph * P] = empty ? 0.0f : m0;
-                    op[PHW + ph * P] = empty ? 0.0f : m1;
-                    ap[ph * P] = empty ? -1 : a0;
-                    ap[PHW + ph * P] = empty ? -1 : a1;
                 }
             }
             k = __builtin_amdgcn_readfirstlane(kn);
@@ -2073,14 +1721,8 @@ FwdWs carve_fwd(void* ws, int64_t R, int N) {
 // resident slot of the CUs the launch stream may use once.
 struct PxPlan {
     int cg = 0, geo_cap = 0, split = 1;
-    int groups = 0;  // > 0: balanced grid of `groups` workgroups (+ 1 for out-of-range batch indices)
     size_t lds = 0;
 };
-// Balanced mode (frcnn_set_path("roi_pool_free_cus", k), k > 0): the grid
-// leaves k of the stream's CUs free and each workgroup's LDS leaves kLeave
-// bytes of its CU for small concurrent kernels (the proposal chain's IoU-tile
-// kernel); images, one 16-, 8- or 4-channel tile per CU.
-constexpr size_t kLeave = 4096;
 PxPlan px_plan(int C, int N, int H, int W, int PHW, hipStream_t st) {
     PxPlan pl;
     const size_t HW = static_cast<size_t>(H) * W;
@@ -2088,24 +1730,10 @@ PxPlan px_plan(int C, int N, int H, int W, int PHW, hipStream_t st) {
     constexpr size_t kReserve = 1024;  // static LDS + allocation rounding
     constexpr size_t kMinGeo = 64 * sizeof(int4);
     const size_t HWs = (HW + 16) & ~static_cast<size_t>(15);  // + the zero sentinel pixel
-    const int free_cus = path_cfg().roi_free_cus;
-    const size_t starts = static_cast<size_t>(N + 1) * sizeof(int);
-    const bool bal = free_cus > 0 && starts <= 16384;
     for (int cg : {16, 8, 4}) {
         if (C % cg != 0) continue;
         if (path_cfg().roi_cg && cg != path_cfg().roi_cg) continue;  // A/B override
         const size_t tile = static_cast<size_t>(cg / 4) * HWs * sizeof(float4);
-        if (bal) {
-            const size_t fixed = tile + starts + kReserve + kLeave;
-            if (fixed + kMinGeo > kLdsPerCu) continue;
-            const size_t geo = (kLdsPerCu - fixed) / sizeof(int4);
-            pl.geo_cap = static_cast<int>(geo > 512 ? 512 : geo);
-            pl.cg = cg;
-            pl.lds = tile + static_cast<size_t>(pl.geo_cap) * sizeof(int4) + starts;
-            const int cus = stream_cu_count(st);
-            pl.groups = cus > free_cus ? cus - free_cus : 1;
-            return pl;
-        }
         int per_cu = 0;
         if (2 * (tile + kMinGeo + kReserve) <= kLdsPerCu) per_cu = 2;
         else if (tile + kMinGeo + kReserve <= kLdsPerCu) per_cu = 1;
@@ -2126,23 +1754,18 @@ PxPlan px_plan(int C, int N, int H, int W, int PHW, hipStream_t st) {
 template <bool HEAD>
 int px_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
               int PH, int PW, float ss, float* out, int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
-    const dim3 grid = pl.groups ? dim3(static_cast<unsigned>(pl.groups + 1))
-                                : dim3(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(pl.split),
-                                       static_cast<unsigned>(N + 1));
+    const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(pl.split), static_cast<unsigned>(N + 1));
     const bool fix7 = PH == 7 && PW == 7;
-#define FRCNN_PX(CG, FX, BAL)                                                                                   \
-    hipLaunchKernelGGL((roi_pool_fwd_wave_kernel<1024, CG, FX, HEAD, BAL>), grid, dim3(1024), pl.lds, st, x,     \
-                       rois, static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd, N)
-#define FRCNN_PX2(CG, FX) \
-    if (pl.groups) FRCNN_PX(CG, FX, true); else FRCNN_PX(CG, FX, false)
+#define FRCNN_PX(CG, FX)                                                                                    \
+    hipLaunchKernelGGL((roi_pool_fwd_wave_kernel<1024, CG, FX, HEAD>), grid, dim3(1024), pl.lds, st, x, rois, \
+                       static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd)
     if (pl.cg == 16) {
-        if (fix7) { FRCNN_PX2(16, 7); } else { FRCNN_PX2(16, 0); }
+        if (fix7) FRCNN_PX(16, 7); else FRCNN_PX(16, 0);
     } else if (pl.cg == 8) {
-        if (fix7) { FRCNN_PX2(8, 7); } else { FRCNN_PX2(8, 0); }
+        if (fix7) FRCNN_PX(8, 7); else FRCNN_PX(8, 0);
     } else {
-        if (fix7) { FRCNN_PX2(4, 7); } else { FRCNN_PX2(4, 0); }
+        if (fix7) FRCNN_PX(4, 7); else FRCNN_PX(4, 0);
     }
-#undef FRCNN_PX2
 #undef FRCNN_PX
     FRCNN_LAUNCH_CHECK("roi_pool_fwd_wave_kernel");
     return FRCNN_OK;
@@ -2154,7 +1777,6 @@ int px_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, in
 // the launch stream's CUs).  CG = 0: does not fit (the wave kernel runs).
 PxPlan pair_plan(int C, int N, int H, int W, int PHW, hipStream_t st) {
     PxPlan pl;
-    if (path_cfg().roi_free_cus > 0 && path_cfg().roi_fwd != kPathPair) return pl;  // balanced: the wave kernel
     const size_t HW = static_cast<size_t>(H) * W;
     if (N <= 0 || HW == 0 || PHW > 64 || W > 255 || HW + 16 > (1 << 22)) return pl;  // flag word: w in 8 bits
     constexpr size_t kReserve = 256;  // static LDS (s_red, s_next) + allocation rounding
@@ -2202,38 +1824,6 @@ int pair_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, 
     }
 #undef FRCNN_PR
     FRCNN_LAUNCH_CHECK("roi_pool_fwd_pair_kernel");
-    return FRCNN_OK;
-}
-
-// Launch plan of the bin-row forward: the 7x7 head with C % 16 == 0 when the
-// image's 16-channel pixel-major tile fits the CU's LDS with room for a
-// RoI-geometry chunk (one workgroup per CU); split as the wave kernel.
-PxPlan row_plan(int C, int N, int H, int W, int PH, int PW, hipStream_t st) {
-    PxPlan pl;
-    const size_t HW = static_cast<size_t>(H) * W;
-    if (N <= 0 || HW == 0 || PH != 7 || PW != 7 || C % 16 != 0) return pl;
-    constexpr size_t kTail = (2 * 16 + 1) * sizeof(int);  // s_red, s_next after the geometry chunk
-    constexpr size_t kMinGeo = 64 * sizeof(int4);
-    const size_t tile = row_tile_bytes(static_cast<int>(HW));
-    if (tile + kMinGeo + kTail > kLdsPerCu) return pl;
-    const size_t geo = (kLdsPerCu - kTail - tile) / sizeof(int4);
-    pl.geo_cap = static_cast<int>(geo > 512 ? 512 : geo);
-    pl.cg = 16;
-    pl.lds = tile + static_cast<size_t>(pl.geo_cap) * sizeof(int4) + kTail;
-    const int64_t wgs = static_cast<int64_t>(C / 16) * N;
-    int64_t sp = (static_cast<int64_t>(stream_cu_count(st)) + wgs - 1) / wgs;
-    if (path_cfg().roi_split > 0) sp = path_cfg().roi_split;  // A/B override
-    pl.split = static_cast<int>(sp < 1 ? 1 : (sp > 64 ? 64 : sp));
-    return pl;
-}
-
-template <bool HEAD>
-int row_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
-               float ss, float* out, int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
-    const dim3 grid(static_cast<unsigned>(C / 16), static_cast<unsigned>(pl.split), static_cast<unsigned>(N + 1));
-    hipLaunchKernelGGL((roi_pool_fwd_row_kernel<1024, HEAD>), grid, dim3(1024), pl.lds, st, x, rois,
-                       static_cast<int>(R), C, H, W, ss, out, argmax, pl.geo_cap, hd);
-    FRCNN_LAUNCH_CHECK("roi_pool_fwd_row_kernel");
     return FRCNN_OK;
 }
 
@@ -2316,8 +1906,6 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
     FRCNN_REQUIRE(x && rois && out && argmax, "frcnn_roi_pool_fwd: null pointer");
     hipStream_t st = as_stream(stream);
     const int path = path_cfg().roi_fwd;
-    const PxPlan rp = (rois_sorted && path == kPathRow) ? row_plan(C, N, H, W, PH, PW, st) : PxPlan{};
-    if (rp.cg) return row_launch<false>(rp, x, rois, R, N, C, H, W, spatial_scale, out, argmax, HeadArgs{}, st);
     const PxPlan pp = (rois_sorted && (path == kPathAuto || path == kPathPair)) ? pair_plan(C, N, H, W, PH * PW, st)
                                                                                : PxPlan{};
     if (pp.cg)
@@ -2367,31 +1955,25 @@ extern "C" int frcnn_roi_pool_fwd_kernel(int64_t R, int N, int C, int H, int W, 
                   "frcnn_roi_pool_fwd_kernel: bad shape");
     hipStream_t st = as_stream(stream);
     const int path = path_cfg().roi_fwd;
-    const bool fix7 = PH == 7 && PW == 7;
-    const int fx = fix7 ? 7 : 0;
+    const int fx = PH == 7 && PW == 7 ? 7 : 0;
     const char* hb = head ? "true" : "false";
     const bool ok = rois_sorted && C > 0;
-    int n = 0;
-    const PxPlan rp = (ok && path == kPathRow) ? row_plan(C, N, H, W, PH, PW, st) : PxPlan{};
-    const PxPlan pp = (!rp.cg && ok && (path == kPathAuto || path == kPathPair)) ? pair_plan(C, N, H, W, PH * PW, st)
-                                                                                : PxPlan{};
-    const PxPlan xp = (!rp.cg && !pp.cg && ok && (path == kPathAuto || path == kPathWave || path == kPathPair))
+    const PxPlan pp = (ok && (path == kPathAuto || path == kPathPair)) ? pair_plan(C, N, H, W, PH * PW, st) : PxPlan{};
+    const PxPlan xp = (!pp.cg && ok && (path == kPathAuto || path == kPathWave || path == kPathPair))
                           ? px_plan(C, N, H, W, PH * PW, st)
                           : PxPlan{};
-    const DensePlan dp = (!rp.cg && !pp.cg && !xp.cg && path != kPathGeneric) ? dense_plan(C, N, H, W, PH * PW)
-                                                                              : DensePlan{};
-    if (rp.cg)
-        n = snprintf(name, len, "roi_pool_fwd_row_kernel<1024, %s>", hb);
-    else if (pp.cg)
+    const DensePlan dp = (!pp.cg && !xp.cg && path != kPathGeneric) ? dense_plan(C, N, H, W, PH * PW) : DensePlan{};
+    int n = 0;
+    if (pp.cg)
         n = snprintf(name, len, "roi_pool_fwd_pair_kernel<1024, %d, %d, %s>", pp.cg, fx, hb);
     else if (xp.cg)
-        n = snprintf(name, len, "roi_pool_fwd_wave_kernel<1024, %d, %d, %s, %s>", xp.cg, fx, hb,
-                     xp.groups ? "true" : "false");
+        n = snprintf(name, len, "roi_pool_fwd_wave_kernel<1024, %d, %d, %s>", xp.cg, fx, hb);
     else if (dp.cg)
         n = snprintf(name, len, "roi_pool_fwd_dense_kernel<1024, %d, %d, %s, %s>", dp.cg, fx,
                      (head && rois_sorted) ? "true" : "false", rois_sorted ? "false" : "true");
     else
-        n = snprintf(name, len, "roi_pool_fwd_kernel<%s>", (static_cast<size_t>(C) * PH * PW) % 4 == 0 ? "true" : "false");
+        n = snprintf(name, len, "roi_pool_fwd_kernel<%s>",
+                     (static_cast<size_t>(C) * PH * PW) % 4 == 0 ? "true" : "false");
     return n < 0 ? FRCNN_EINVAL : FRCNN_OK;
 }
 
@@ -2408,14 +1990,6 @@ extern "C" int frcnn_roi_pool_fwd_head(const float* x, const float* rois, const 
     FRCNN_REQUIRE(rois && roi_inds && boxes, "frcnn_roi_pool_fwd_head: null pointer");
     const int path = path_cfg().roi_fwd;
     const bool aligned = reinterpret_cast<uintptr_t>(rois) % 16 == 0;
-    const PxPlan rp = (rois_sorted && C > 0 && aligned && path == kPathRow)
-                          ? row_plan(C, N, H, W, PH, PW, as_stream(stream))
-                          : PxPlan{};
-    if (rp.cg) {  // transform + pack inside the pool kernel
-        FRCNN_REQUIRE(x && out && argmax, "frcnn_roi_pool_fwd_head: null pointer");
-        const HeadArgs hd{roi_inds, img_h, img_w, static_cast<float>(H), static_cast<float>(W), boxes};
-        return row_launch<true>(rp, x, rois, R, N, C, H, W, spatial_scale, out, argmax, hd, as_stream(stream));
-    }
     const PxPlan pp = (rois_sorted && C > 0 && aligned && (path == kPathAuto || path == kPathPair))
                           ? pair_plan(C, N, H, W, PH * PW, as_stream(stream))
                           : PxPlan{};

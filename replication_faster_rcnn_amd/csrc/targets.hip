@@ -73,7 +73,6 @@ __global__ __launch_bounds__(64) void gt_compact_kernel(const double* __restrict
                                                         int Gp, double* __restrict__ gt,
                                                         double* __restrict__ gl,
                                                         int* __restrict__ gcount) {
-    latency_prio();
     const int n = blockIdx.x, lane = threadIdx.x;
     int base = 0;
     for (int g0 = 0; g0 < Gp; g0 += 64) {
@@ -116,7 +115,6 @@ __global__ __launch_bounds__(256) void at_iou_kernel(const float* __restrict__ a
                                                      double* __restrict__ row_max,
                                                      double* __restrict__ col_v,
                                                      int* __restrict__ col_i) {
-    latency_prio();
     __shared__ double sg[kMaxG][4];
     __shared__ double sa[kMaxG];
     __shared__ ArgMax wred[4][kMaxG];
@@ -178,7 +176,6 @@ __global__ __launch_bounds__(1024) void at_label_kernel(
     const double* __restrict__ col_v, const int* __restrict__ col_i, double neg_thr, double pos_thr,
     int32_t* __restrict__ row_arg, int8_t* __restrict__ label0, int* __restrict__ pos_list,
     int* __restrict__ neg_list, int* __restrict__ npos, int* __restrict__ nneg) {
-    latency_prio();
     __shared__ int s_garg[kMaxG];
     __shared__ int s_w[16];
     const int n = blockIdx.x;
@@ -614,7 +611,6 @@ __global__ __launch_bounds__(kSampThreads) void at_sample_kernel(
     int N, int A, int n_sample, int n_pos_max, const int* __restrict__ pos_list,
     const int* __restrict__ neg_list, const int* __restrict__ npos, const int* __restrict__ nneg,
     uint32_t* __restrict__ rng, uint8_t* __restrict__ keep, int* __restrict__ sampled) {
-    latency_prio();
     __shared__ WalkLds S;
     __shared__ int J[kMaxKeep];
     __shared__ FinalLds FL;
@@ -653,7 +649,6 @@ __global__ __launch_bounds__(256) void at_finish_kernel(
     const int* __restrict__ gcount, int Gp, const int32_t* __restrict__ row_arg,
     const int8_t* __restrict__ label0, const uint8_t* __restrict__ keep,
     const int* __restrict__ sampled, int32_t* __restrict__ label, double* __restrict__ reg) {
-    latency_prio();
     const int n = blockIdx.y;
     const int a = blockIdx.x * 256 + threadIdx.x;
     if (a >= A) return;
@@ -695,7 +690,6 @@ __global__ __launch_bounds__(1024) void pt_iou_kernel(
     int Gp, double pos_thr, double neg_hi, double neg_lo, double* __restrict__ roi_all,
     int32_t* __restrict__ assign, int* __restrict__ pos_list, int* __restrict__ neg_list,
     int* __restrict__ npos, int* __restrict__ nneg) {
-    latency_prio();
     __shared__ double sg[kMaxG][4];
     __shared__ double sa[kMaxG];
     __shared__ int s_w[16];
@@ -772,7 +766,6 @@ __global__ __launch_bounds__(kSampThreads) void pt_sample_kernel(
     const int* __restrict__ neg_list, const int* __restrict__ npos, const int* __restrict__ nneg,
     uint32_t* __restrict__ rng, int* __restrict__ sample, int* __restrict__ scount,
     int* __restrict__ spos) {
-    latency_prio();
     __shared__ WalkLds S;
     __shared__ int J[kMaxKeep];
     __shared__ FinalLds FL;
@@ -816,7 +809,6 @@ __global__ __launch_bounds__(128) void pt_finish_kernel(
     int Gp, const int* __restrict__ sample, const int* __restrict__ scount,
     const int* __restrict__ spos, RegNorm nrm, double* __restrict__ s_roi, double* __restrict__ s_reg,
     double* __restrict__ s_lab) {
-    latency_prio();
     const int n = blockIdx.x;
     const int s = threadIdx.x + blockIdx.y * 128;
     if (s >= n_sample) return;
@@ -855,7 +847,6 @@ template <class TA, class TB, class TO>
 __global__ __launch_bounds__(256) void bbox_iou_kernel(const TA* __restrict__ a, int64_t na,
                                                        const TB* __restrict__ b, int64_t nb,
                                                        TO* __restrict__ out) {
-    latency_prio();
     const int64_t idx = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
     if (idx >= na * nb) return;
     const int64_t i = idx / nb, j = idx - i * nb;
@@ -885,7 +876,6 @@ template <class TA, class TB>
 __global__ __launch_bounds__(256) void bbox2reg_kernel(const TA* __restrict__ a,
                                                        const TB* __restrict__ b, int64_t n,
                                                        double* __restrict__ out) {
-    latency_prio();
     const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
     if (i >= n) return;
     const TA* p = a + i * 4;

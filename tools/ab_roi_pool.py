@@ -2,7 +2,7 @@
 
     python tools/ab_roi_pool.py [--config cfg2] [--variants blocks,blocks:4,dense@3,dense/u,generic]
 
-A variant is `path[:cg][@split][%free_cus][/u]`: path = blocks | dense | generic
+A variant is `path[:cg][@split][/u]`: path = blocks | dense | generic
 (frcnn_set_path("roi_pool_fwd", path)), cg = channels per workgroup
 ("roi_pool_cg"), split = RoI / unit shares per image ("roi_pool_split"), /u =
 RoIs passed as unsorted (per-image lists first).
@@ -58,10 +58,8 @@ def main():
     for rnd in range(a.rounds):
         for vs in variants:
             v, uns = (vs[:-2], True) if vs.endswith("/u") else (vs, False)
-            v, _, fr = v.partition("%")
             v, _, sp = v.partition("@")
             v, _, cg = v.partition(":")
-            _lib.set_path("roi_pool_free_cus", fr or "0")
             _lib.set_path("roi_pool_split", sp or "auto")
             _lib.set_path("roi_pool_cg", cg or "auto")
             _lib.set_path("roi_pool_fwd", v)
@@ -78,7 +76,7 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             times[vs].append(e0.elapsed_time(e1) / a.iters * 1e3)
-    for op in ("roi_pool_split", "roi_pool_cg", "roi_pool_fwd", "roi_pool_free_cus"):
+    for op in ("roi_pool_split", "roi_pool_cg", "roi_pool_fwd"):
         _lib.set_path(op, "auto")
     res = {v: {"us_median": float(np.median(t)), "us_min": float(np.min(t)),
                "GBps": alg / (np.median(t) * 1e-6) / 1e9} for v, t in times.items()}

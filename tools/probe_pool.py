@@ -29,11 +29,9 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--path", default="auto", help="frcnn_set_path roi_pool_fwd")
-    ap.add_argument("--free", default="0", help="frcnn_set_path roi_pool_free_cus")
     a = ap.parse_args()
     lib = _lib.load()
     _lib.set_path("roi_pool_fwd", a.path)
-    _lib.set_path("roi_pool_free_cus", a.free)
     fn = lib.frcnn_debug_pool_prof
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
