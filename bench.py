@@ -90,6 +90,8 @@ def parse():
                          "gloo (host copies) when ranks share one")
     ap.add_argument("--roi-cg", default="auto",
                     help="channels per RoIPool forward workgroup (frcnn_set_path roi_pool_cg): auto | 4 | 8 | 16")
+    ap.add_argument("--roi-path", default="auto",
+                    help="RoIPool forward kernel (frcnn_set_path roi_pool_fwd): auto | pair | wave | dense | generic")
     ap.add_argument("--roi-split", default="auto",
                     help="RoI shares per (image, channel group) of the RoIPool forward "
                          "(frcnn_set_path roi_pool_split): auto | 1 | 2 | ...")
@@ -596,7 +598,7 @@ def main():
     from replication_faster_rcnn_amd import _lib
     from replication_faster_rcnn_amd import anchors as A
     for op, v in (("roi_pool_cg", args.roi_cg), ("roi_pool_split", args.roi_split),
-                  ("propose", args.propose_path)):
+                  ("roi_pool_fwd", args.roi_path), ("propose", args.propose_path)):
         if v != "auto":
             _lib.set_path(op, v)
     from replication_faster_rcnn_amd import dist as fdist
@@ -709,7 +711,7 @@ def main():
                    "parallelism": f"dp{world} (per-image sharding)", "streams": args.streams,
                    "prop_streams": args.prop_streams if (args.streams == 2 and not train) else 1,
                    "pool_on": args.pool_on if (args.streams == 2 and not train) else None,
-                   "host_io": bool(args.host_io), "roi_cg": args.roi_cg, "roi_split": args.roi_split,
+                   "host_io": bool(args.host_io), "roi_path": args.roi_path, "roi_cg": args.roi_cg, "roi_split": args.roi_split,
                    "prop_cus": args.prop_cus if (args.streams == 2 and not train) else 0,
                    "propose_path": args.propose_path,
                    "collective": (None if world == 1 else

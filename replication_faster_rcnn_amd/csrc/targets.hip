@@ -449,12 +449,12 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
         // The first wave whose exact base (prefix of the counts before it) falls
         // outside its margins, and every wave after it, re-solves next round with
         // the new prefix; the waves before it are settled.  Counts hardly depend on
-        // the base, so the second round's bases are nearly exact and most windows
-        // settle there; each round settles at least one more wave.
+        // the base, so the first round's guesses are usually inside the margins and
+        // the rest settle in the second; each round settles at least one more wave.
         int il = 0, total = 0, par = 0;
         uint32_t m = 0;
         bool a = false, done = wid >= kWinWaves;  // the twisting waves only keep the barriers
-        for (int round = 0;; ++round) {
+        for (;;) {  // rounds
             if (!done) {
                 for (;;) {  // this wave's 64 words, exact for the assumed `base`
                     const int below = static_cast<int>(__builtin_amdgcn_mbcnt_hi(
@@ -468,11 +468,12 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
                     acc = nacc;
                 }
             }
-            // Margins only from the second round on: the first round's bases are
-            // guesses, so it settles just the waves whose guess was exact (d == 0);
-            // settled waves keep d == 0 and need none either.
+            // Margins from the first round on: a wave's 64-word pattern depends on its
+            // base only where (w & mask) lies that close to the step, so at wide
+            // masks the guessed bases usually fall inside the margins and the window
+            // settles in one round (settled waves keep d == 0 and need none).
             uint32_t dn = 0, up = 0;
-            if (round > 0 && !done) {
+            if (!done) {
                 if (il < 1) {
                     dn = 0x3fffffffu;
                     up = static_cast<uint32_t>(-il);
