@@ -21,7 +21,7 @@ GPU and exits with its code.  Images are seeded by global index, so every
 rank's shard is the same data as in the 1-GPU run.
 
 Each step's proposal layer and RoIPool run back to back on one HIP stream, and
-consecutive steps alternate over --prop-streams (3) streams, so step k+1's
+consecutive steps alternate over --prop-streams (4) streams, so step k+1's
 proposals run beside step k's RoIPool without cross-stream waits (--streams 1
 serialises everything; --pool-on own puts the RoIPool on a stream of its own).
 Every step does all of its work.
@@ -33,9 +33,16 @@ this host's cores, rank 0 at N=1 only).
 """
 from __future__ import annotations
 
+import os
+
+# HIP hardware queues for this process (HIP's default is 4, one of them taken by
+# torch's default stream): the four step streams get a queue each instead of two
+# of them sharing one (cfg2: 98.4k vs 96.2k images/s at 300 steps, 91.3k vs
+# 86.9k at 20; profiles/r3_experiments.md).  Must be set before HIP initialises.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 import argparse
 import json
-import os
 import socket
 import subprocess
 import sys
@@ -63,7 +70,7 @@ def parse():
     ap.add_argument("--streams", type=int, default=2, choices=(1, 2),
                     help="2: the proposal layer of step k+1 runs on its own HIP stream beside "
                          "step k's RoIPool (each step still does all of its work)")
-    ap.add_argument("--prop-streams", type=int, default=3,
+    ap.add_argument("--prop-streams", type=int, default=4,
                     help="with --streams 2 (inference configs): proposal layers of consecutive "
                          "steps round-robin over this many HIP streams")
     ap.add_argument("--pool-on", default="prop", choices=("prop", "own"),

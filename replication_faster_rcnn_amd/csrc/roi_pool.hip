@@ -1906,8 +1906,10 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
     FRCNN_REQUIRE(x && rois && out && argmax, "frcnn_roi_pool_fwd: null pointer");
     hipStream_t st = as_stream(stream);
     const int path = path_cfg().roi_fwd;
-    const PxPlan pp = (rois_sorted && (path == kPathAuto || path == kPathPair)) ? pair_plan(C, N, H, W, PH * PW, st)
-                                                                               : PxPlan{};
+    // the pair-tile kernel only on request: alone it matches the wave kernel
+    // (64.9-70.1 vs 67.1-69.2 us at cfg2), beside other steps' kernels it loses
+    // (cfg2 bench 88.8-91.1k vs 94.4-97.6k images/s, cfg1 9.4k vs 10.1k)
+    const PxPlan pp = (rois_sorted && path == kPathPair) ? pair_plan(C, N, H, W, PH * PW, st) : PxPlan{};
     if (pp.cg)
         return pair_launch<false>(pp, x, rois, R, N, C, H, W, PH, PW, spatial_scale, out, argmax, HeadArgs{}, st);
     const PxPlan xp = (rois_sorted && (path == kPathAuto || path == kPathWave || path == kPathPair))
@@ -1958,7 +1960,7 @@ extern "C" int frcnn_roi_pool_fwd_kernel(int64_t R, int N, int C, int H, int W, 
     const int fx = PH == 7 && PW == 7 ? 7 : 0;
     const char* hb = head ? "true" : "false";
     const bool ok = rois_sorted && C > 0;
-    const PxPlan pp = (ok && (path == kPathAuto || path == kPathPair)) ? pair_plan(C, N, H, W, PH * PW, st) : PxPlan{};
+    const PxPlan pp = (ok && path == kPathPair) ? pair_plan(C, N, H, W, PH * PW, st) : PxPlan{};
     const PxPlan xp = (!pp.cg && ok && (path == kPathAuto || path == kPathWave || path == kPathPair))
                           ? px_plan(C, N, H, W, PH * PW, st)
                           : PxPlan{};
@@ -1990,7 +1992,7 @@ extern "C" int frcnn_roi_pool_fwd_head(const float* x, const float* rois, const 
     FRCNN_REQUIRE(rois && roi_inds && boxes, "frcnn_roi_pool_fwd_head: null pointer");
     const int path = path_cfg().roi_fwd;
     const bool aligned = reinterpret_cast<uintptr_t>(rois) % 16 == 0;
-    const PxPlan pp = (rois_sorted && C > 0 && aligned && (path == kPathAuto || path == kPathPair))
+    const PxPlan pp = (rois_sorted && C > 0 && aligned && path == kPathPair)
                           ? pair_plan(C, N, H, W, PH * PW, as_stream(stream))
                           : PxPlan{};
     if (pp.cg) {  // transform + pack inside the pool kernel
