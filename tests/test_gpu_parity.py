@@ -249,7 +249,7 @@ def test_propose_edge_cases(case, path):
 
 
 # forward paths: (kernel path, RoIs promised grouped by image)
-FWD_PATHS = [("wave", True), ("dense", True), ("dense", False), ("generic", False)]
+FWD_PATHS = [("wave", True), ("pair", True), ("dense", True), ("dense", False), ("generic", False)]
 
 
 def _special_x(r, N=2, C=16, H=12, W=14):
@@ -317,7 +317,7 @@ def _rand_rois(r, b, H, W, lo=-3, span=40):
     return np.concatenate([np.asarray(b, np.float32)[:, None], xy, xy + wh], 1).astype(np.float32)
 
 
-@pytest.mark.parametrize("fpath", ["wave", "dense"])
+@pytest.mark.parametrize("fpath", ["wave", "pair", "dense"])
 @pytest.mark.parametrize("split", ["auto", "1", "3", "64"])
 @pytest.mark.parametrize("case", ["many_images", "invalid_ends", "unsorted", "single_roi", "gaps",
                                   "one_image_tiny_rois", "uniform_sizes", "ph5", "ph8x8", "ph3x9",
@@ -633,3 +633,17 @@ def test_roi_pool_bwd_poisoned_workspace(path):
                            torch.from_numpy(oa).to(DEV), x.shape, 1.0)
         torch.cuda.synchronize()
     assert np.array_equal(gi.cpu().numpy(), ref)
+
+
+def test_roi_pool_fwd_kernel_label():
+    """frcnn_roi_pool_fwd_kernel names what frcnn_roi_pool_fwd(_head) launches:
+    the wave kernel by default for RoIs grouped by image, the pair-tile kernel
+    on request, the dense kernel for unsorted RoIs (bench.py's roofline label)."""
+    R, N, C, H, W = 2400, 8, 256, 38, 63
+    assert _lib.roi_pool_fwd_kernel(R, N, C, H, W) == "roi_pool_fwd_wave_kernel<1024, 16, 7, true>"
+    assert _lib.roi_pool_fwd_kernel(R, N, C, H, W, head=False) == "roi_pool_fwd_wave_kernel<1024, 16, 7, false>"
+    assert _lib.roi_pool_fwd_kernel(2000, 1, 512, 50, 84) == "roi_pool_fwd_wave_kernel<1024, 8, 7, true>"
+    with _lib.kernel_path("roi_pool_fwd", "pair"):
+        assert _lib.roi_pool_fwd_kernel(R, N, C, H, W) == "roi_pool_fwd_pair_kernel<1024, 8, 7, true>"
+    assert _lib.roi_pool_fwd_kernel(R, N, C, H, W, rois_sorted=False, head=False).startswith(
+        "roi_pool_fwd_dense_kernel<1024, 16, 7, false, true>")
