@@ -38,8 +38,10 @@ import os
 # HIP hardware queues for this process (HIP's default is 4, one of them taken by
 # torch's default stream): the four step streams get a queue each instead of two
 # of them sharing one (cfg2: 98.4k vs 96.2k images/s at 300 steps, 91.3k vs
-# 86.9k at 20; profiles/r3_experiments.md).  Must be set before HIP initialises.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# 86.9k at 20; with 4 queues and 4 streams 85.9k / 79.3k; profiles/r3_experiments.md).
+# Set before HIP initialises, over an environment that pins HIP's default 4
+# (FRCNN_BENCH_HW_QUEUES overrides the bench's choice).
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("FRCNN_BENCH_HW_QUEUES", "8")
 
 import argparse
 import json
