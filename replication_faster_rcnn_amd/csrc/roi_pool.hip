@@ -1012,12 +1012,10 @@ __global__ __launch_bounds__(256) void roi_transform_kernel(const float* __restr
 // `code` (optional, the backward prep's per-bin codes): entries of RoIs whose
 // bin 0 code has the "slow" bit (overlaps beyond the grid neighbours) get bit
 // 31 set, so the leader backward learns a RoI's path from the scalar list load.
-__global__ __launch_bounds__(1024) void roi_lists_kernel(const float* __restrict__ rois, int R,
-                                                         int N, int* __restrict__ list,
-                                                         int* __restrict__ cnt, int stride = 5,
-                                                         const uint8_t* __restrict__ code = nullptr,
-                                                         int PHW = 0) {
-    const int b = blockIdx.x;
+template <class Flag>
+__device__ __forceinline__ void roi_lists_image(const float* __restrict__ rois, int R, int N, int b,
+                                                int* __restrict__ list, int* __restrict__ cnt, int stride,
+                                                Flag flag_of) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     __shared__ int s_w[16];
     __shared__ int s_last;
@@ -1035,7 +1033,7 @@ __global__ __launch_bounds__(1024) void roi_lists_kernel(const float* __restrict
             tot += s_w[w];
         }
         if (m) {
-            const int flag = code ? (code[static_cast<size_t>(r) * PHW] & 16) << 27 : 0;
+            const int flag = flag_of(r) ? static_cast<int>(0x80000000u) : 0;
             const int pos = base + before + __popcll(bal & lanemask_lt());
             list[static_cast<size_t>(b) * list_stride(R) + pos] = r | flag;
             if (pos == base + tot - 1) s_last = r | flag;
@@ -1047,6 +1045,15 @@ __global__ __launch_bounds__(1024) void roi_lists_kernel(const float* __restrict
     // kListPad entries past the last one repeat it, so a reader may fetch whole
     // groups of entries past the image's count without bounds checks
     if (tid < kListPad) list[static_cast<size_t>(b) * list_stride(R) + base + tid] = base > 0 ? s_last : 0;
+}
+
+__global__ __launch_bounds__(1024) void roi_lists_kernel(const float* __restrict__ rois, int R,
+                                                         int N, int* __restrict__ list,
+                                                         int* __restrict__ cnt, int stride = 5,
+                                                         const uint8_t* __restrict__ code = nullptr,
+                                                         int PHW = 0) {
+    roi_lists_image(rois, R, N, blockIdx.x, list, cnt, stride,
+                    [&](int r) { return code && (code[static_cast<size_t>(r) * PHW] & 16); });
 }
 
 // Outputs of RoIs with an out-of-range batch index: 0 / -1 (torchvision: UB);
@@ -1140,13 +1147,10 @@ __global__ __launch_bounds__(256) void roi_bwd_prep_kernel(const float* __restri
 // bin.  Bin windows are separable (rows depend on ph only, columns on pw only),
 // so a bin's overlap set is (rows overlapping its row) x (columns overlapping
 // its column): PH + PW lane reads instead of a walk over every earlier bin.
-__global__ __launch_bounds__(256) void roi_bwd_prep64_kernel(const float* __restrict__ rois, int R,
-                                                             int H, int W, int PH, int PW, float ss,
-                                                             uint64_t* __restrict__ cmask,
-                                                             uint8_t* __restrict__ code) {
+__device__ __forceinline__ void roi_bwd_prep64_roi(const float* __restrict__ rois, int r, int H, int W, int PH,
+                                                   int PW, float ss, uint64_t* __restrict__ cmask,
+                                                   uint8_t* __restrict__ code) {
     const int lane = threadIdx.x & 63;
-    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r >= R) return;  // whole wave
     const int PHW = PH * PW;
     const float* roi = rois + static_cast<size_t>(r) * 5;
     const int k = lane < PHW ? lane : 0;
@@ -1190,6 +1194,58 @@ __global__ __launch_bounds__(256) void roi_bwd_prep64_kernel(const float* __rest
     }
     const bool slow = __ballot(other) != 0;
     if (lane < PHW) code[static_cast<size_t>(r) * PHW + lane] = static_cast<uint8_t>(nb | (slow ? 16u : 0u));
+}
+
+__global__ __launch_bounds__(256) void roi_bwd_prep64_kernel(const float* __restrict__ rois, int R,
+                                                             int H, int W, int PH, int PW, float ss,
+                                                             uint64_t* __restrict__ cmask,
+                                                             uint8_t* __restrict__ code) {
+    const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= R) return;  // whole wave
+    roi_bwd_prep64_roi(rois, r, H, W, PH, PW, ss, cmask, code);
+}
+
+// Whether a RoI's bins can overlap beyond their grid neighbours: some bin row
+// overlaps the row two below it, or some bin column the column two right of it
+// (windows are separable and monotone).  A superset of the prep kernel's
+// per-RoI "slow" flag (which also looks at emptiness), so a RoI it clears has
+// only neighbour overlaps -- the leader backward's precondition; flagged RoIs
+// take the exact ranked path either way.
+__device__ __forceinline__ bool roi_far_overlap(const float* __restrict__ roi, float ss, int H, int W, int PH,
+                                                int PW) {
+    const RoiGeom g = roi_geom(roi, ss, PH, PW);
+    bool far = false;
+    for (int q = 0; q + 2 < PH; ++q) {
+        const int4 a = geom_bin(g, H, W, q, 0), c = geom_bin(g, H, W, q + 2, 0);
+        far |= a.y > c.x && a.y > a.x && c.y > c.x;
+    }
+    for (int q = 0; q + 2 < PW; ++q) {
+        const int4 a = geom_bin(g, H, W, 0, q), c = geom_bin(g, H, W, 0, q + 2);
+        far |= a.w > c.z && a.w > a.z && c.w > c.z;
+    }
+    return far;
+}
+
+// The leader backward's two preparations in one launch (PH*PW <= 64): workgroups
+// [0, N] build the per-image RoI lists, their entries flagged from the RoI
+// geometry (roi_far_overlap); the others compute the per-RoI overlap masks and
+// codes (16 RoIs per workgroup, one wave each).  Independent, so one launch
+// instead of two back to back.
+__global__ __launch_bounds__(1024) void roi_bwd_prep_lists_kernel(const float* __restrict__ rois, int R, int N,
+                                                                  int H, int W, int PH, int PW, float ss,
+                                                                  uint64_t* __restrict__ cmask,
+                                                                  uint8_t* __restrict__ code,
+                                                                  int* __restrict__ list, int* __restrict__ cnt) {
+    const int b = blockIdx.x;
+    if (b <= N) {
+        roi_lists_image(rois, R, N, b, list, cnt, 5, [&](int r) {
+            return roi_far_overlap(rois + static_cast<size_t>(r) * 5, ss, H, W, PH, PW);
+        });
+        return;
+    }
+    const int r = (b - N - 1) * 16 + (threadIdx.x >> 6);
+    if (r >= R) return;  // whole wave
+    roi_bwd_prep64_roi(rois, r, H, W, PH, PW, ss, cmask, code);
 }
 
 // General plane-owner backward (any output size; planes in LDS or, when a
@@ -1485,7 +1541,7 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
         int am_r[D], fl_r[D];
         float g_r[D];
         uint32_t cl_r[D], ch_r[D];
-        // list entries: RoI index | flag << 31 (roi_lists_kernel with the codes);
+        // list entries: RoI index | flag << 31 (roi_bwd_prep_lists_kernel);
         // the flag drops out of the byte offsets (index x an even stride, mod
         // 2^32).  Positions past the image's RoIs hold copies of its last entry
         // (kListPad of them: a raw buffer load's soffset is not range-checked,
@@ -2076,13 +2132,6 @@ extern "C" int frcnn_roi_pool_bwd(const float* grad, const float* rois, const in
     FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_bwd: workspace %zu < %zu",
                   ws_bytes, w.bytes);
     FRCNN_REQUIRE(N <= 65535, "frcnn_roi_pool_bwd: N > 65535");
-    if (PH * PW <= 64)
-        hipLaunchKernelGGL(roi_bwd_prep64_kernel, dim3(static_cast<unsigned>((R + 3) / 4)), dim3(256), 0, st,
-                           rois, static_cast<int>(R), H, W, PH, PW, spatial_scale, w.cmask, w.code);
-    else
-        hipLaunchKernelGGL(roi_bwd_prep_kernel, dim3(static_cast<unsigned>(R)), dim3(256), 0, st, rois,
-                           H, W, PH, PW, spatial_scale, w.cmask, w.code);
-    FRCNN_LAUNCH_CHECK("roi_bwd_prep_kernel");
     const size_t plane_bytes = HW * sizeof(float);
     const int PHW = PH * PW;
     const int bp = path_cfg().roi_bwd;
@@ -2109,10 +2158,23 @@ extern "C" int frcnn_roi_pool_bwd(const float* grad, const float* rois, const in
         lead_bytes = static_cast<size_t>(icpw) * (HWs * sizeof(float) + 2 * kBwdXRow * 8);
         lead = fits && bp == kPathAuto && PHW < 64 && PW == 7 && lead_bytes <= kPlaneBudgetRing;
     }
-    // the leader kernel reads each RoI's path flag from its list entry
-    hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, rois, static_cast<int>(R), N, w.list,
-                       w.cnt, 5, lead ? w.code : nullptr, PHW);
-    FRCNN_LAUNCH_CHECK("roi_lists_kernel");
+    if (lead) {  // lists (entries flagged from the geometry) and masks / codes in one launch
+        const unsigned grid = static_cast<unsigned>(N + 1 + (R + 15) / 16);
+        hipLaunchKernelGGL(roi_bwd_prep_lists_kernel, dim3(grid), dim3(1024), 0, st, rois, static_cast<int>(R), N, H,
+                           W, PH, PW, spatial_scale, w.cmask, w.code, w.list, w.cnt);
+        FRCNN_LAUNCH_CHECK("roi_bwd_prep_lists_kernel");
+    } else {
+        if (PHW <= 64)
+            hipLaunchKernelGGL(roi_bwd_prep64_kernel, dim3(static_cast<unsigned>((R + 3) / 4)), dim3(256), 0, st,
+                               rois, static_cast<int>(R), H, W, PH, PW, spatial_scale, w.cmask, w.code);
+        else
+            hipLaunchKernelGGL(roi_bwd_prep_kernel, dim3(static_cast<unsigned>(R)), dim3(256), 0, st, rois,
+                               H, W, PH, PW, spatial_scale, w.cmask, w.code);
+        FRCNN_LAUNCH_CHECK("roi_bwd_prep_kernel");
+        hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, rois, static_cast<int>(R), N, w.list,
+                           w.cnt, 5, nullptr, PHW);
+        FRCNN_LAUNCH_CHECK("roi_lists_kernel");
+    }
     if (ring) {
         dim3 grid((C + icpw - 1) / icpw, N);
         if (lead)
