@@ -544,6 +544,15 @@ def train_step_fn(args, c, sets, base, first_image, ev):
     prep_ready = [torch.cuda.Event() for _ in range(2)]
     sample_done = [None, None]
     sample_ev = [torch.cuda.Event() for _ in range(2)]
+    # ProposalTargetCreator's RNG-free half (IoU, fg / bg lists) follows the
+    # proposals on their stream; the draws' stream only runs the draws
+    pt_ws = [targets.proposal_targets_workspace(N, c["post_nms"], boxes.size(1), S, dev) for _ in range(2)]
+    pt_out = [(torch.empty((N, S, 4), dtype=torch.float64, device=dev),
+               torch.empty((N, S, 4), dtype=torch.float64, device=dev),
+               torch.empty((N, S), dtype=torch.float64, device=dev),
+               torch.empty((N,), dtype=torch.int32, device=dev)) for _ in range(2)]
+    pt_done = [None, None]
+    pt_ev = [torch.cuda.Event() for _ in range(2)]
     k_step = [0]
 
     def step(timed):
@@ -559,6 +568,9 @@ def train_step_fn(args, c, sets, base, first_image, ev):
             rois, _, cnt = ops.propose(sc, de, img_w=c["img_w"], img_h=c["img_h"],
                                        pre_nms=c["pre_nms"], post_nms=c["post_nms"],
                                        anchor_base=base, feat_h=c["feat_h"], feat_w=c["feat_w"])
+            if pt_done[j] is not None:
+                s_prop.wait_event(pt_done[j])  # the draws that read pt_ws[j] last time
+            pplan = targets.proposal_targets_prepare(rois, cnt, boxes, labels, n_sample=S, workspace=pt_ws[j])
             prop_ready = torch.cuda.Event()
             prop_ready.record(s_prop)
         with torch.cuda.stream(s_rng):
@@ -567,10 +579,9 @@ def train_step_fn(args, c, sets, base, first_image, ev):
             sample_ev[j].record(s_rng)
             sample_done[j] = sample_ev[j]
             s_rng.wait_event(prop_ready)
-            rois.record_stream(s_rng)   # allocated on s_prop, read on s_rng
-            cnt.record_stream(s_rng)
-            s_roi, s_reg, s_lab, s_cnt = targets.proposal_targets(rois, cnt, boxes, labels,
-                                                                  n_sample=S, rng=rng)
+            s_roi, s_reg, s_lab, s_cnt = targets.proposal_targets_sample(pplan, rng=rng, out=pt_out[j])
+            pt_ev[j].record(s_rng)
+            pt_done[j] = pt_ev[j]
             sample_rois = s_roi.float().view(-1, 4)          # train.py:86,102,107
             ready = torch.cuda.Event()
             ready.record(s_rng)

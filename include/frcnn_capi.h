@@ -247,6 +247,21 @@ int frcnn_proposal_target(int N, int Rp, const float* rois, const int32_t* rcoun
                           const double* reg_std, uint32_t* rng_state, double* sample_roi,
                           double* gt_roi_reg, double* gt_roi_label, int32_t* sample_count,
                           void* workspace, size_t ws_bytes, void* stream);
+/* frcnn_proposal_target in two halves on one workspace (same arguments):
+ *   _prepare: utils/utils.py:221-246 (gt concat, IoU, argmax, fg / bg lists) --
+ *             no RNG, so it can run on the proposals' stream, off the draws' stream;
+ *   _sample:  utils/utils.py:248-276 (the np.random.choice draws on rng_state,
+ *             sample order, regression targets); runs after prepare on the same
+ *             workspace (order the streams with an event). */
+int frcnn_proposal_target_prepare(int N, int Rp, const float* rois, const int32_t* rcount, int G,
+                                  const double* boxes, const double* labels, int n_sample,
+                                  double pos_iou_thresh, double neg_iou_thresh_high,
+                                  double neg_iou_thresh_low, void* workspace, size_t ws_bytes,
+                                  void* stream);
+int frcnn_proposal_target_sample(int N, int Rp, int G, int n_sample, double pos_ratio,
+                                 const double* reg_mean, const double* reg_std, uint32_t* rng_state,
+                                 double* sample_roi, double* gt_roi_reg, double* gt_roi_label,
+                                 int32_t* sample_count, void* workspace, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

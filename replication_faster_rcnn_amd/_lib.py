@@ -73,6 +73,8 @@ SIGNATURES = {
     "frcnn_proposal_target_workspace_size": (SZ, [I32, I32, I32, I32]),
     "frcnn_proposal_target": (I32, [I32, I32, P, P, I32, P, P, I32, F64, F64, F64, F64, P, P, P,
                                     P, P, P, P, P, SZ, P]),
+    "frcnn_proposal_target_prepare": (I32, [I32, I32, P, P, I32, P, P, I32, F64, F64, F64, P, SZ, P]),
+    "frcnn_proposal_target_sample": (I32, [I32, I32, I32, I32, F64, P, P, P, P, P, P, P, P, SZ, P]),
 }
 
 # diagnostic entry points of instrumented builds only (not in include/frcnn_capi.h)

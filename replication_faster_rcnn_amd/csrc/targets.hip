@@ -1085,20 +1085,15 @@ extern "C" size_t frcnn_proposal_target_workspace_size(int N, int Rp, int G, int
     return carve_pt(nullptr, N, Rp, G > 0 ? G : 1, n_sample).bytes;
 }
 
-extern "C" int frcnn_proposal_target(int N, int Rp, const float* rois, const int32_t* rcount, int G,
-                                     const double* boxes, const double* labels, int n_sample,
-                                     double pos_ratio, double pos_iou_thresh,
-                                     double neg_iou_thresh_high, double neg_iou_thresh_low,
-                                     const double* reg_mean, const double* reg_std,
-                                     uint32_t* rng_state, double* sample_roi, double* gt_roi_reg,
-                                     double* gt_roi_label, int32_t* sample_count, void* workspace,
-                                     size_t ws_bytes, void* stream) {
+extern "C" int frcnn_proposal_target_prepare(int N, int Rp, const float* rois, const int32_t* rcount, int G,
+                                             const double* boxes, const double* labels, int n_sample,
+                                             double pos_iou_thresh, double neg_iou_thresh_high,
+                                             double neg_iou_thresh_low, void* workspace, size_t ws_bytes,
+                                             void* stream) {
     FRCNN_REQUIRE(N > 0 && N <= 65535 && Rp >= 0 && G >= 0 && G <= kMaxG && n_sample > 0,
                   "frcnn_proposal_target: bad shape");
     FRCNN_REQUIRE(Rp + G <= kMaxKeep, "frcnn_proposal_target: rois + gt must be <= %d", kMaxKeep);
-    FRCNN_REQUIRE(rcount && rng_state && sample_roi && gt_roi_reg && gt_roi_label && sample_count &&
-                      reg_mean && reg_std,
-                  "frcnn_proposal_target: null pointer");
+    FRCNN_REQUIRE(rcount, "frcnn_proposal_target: null pointer");
     FRCNN_REQUIRE(Rp == 0 || rois, "frcnn_proposal_target: null rois");
     FRCNN_REQUIRE(G == 0 || (boxes && labels), "frcnn_proposal_target: null boxes");
     const int Gp = G > 0 ? G : 1;
@@ -1113,11 +1108,29 @@ extern "C" int frcnn_proposal_target(int N, int Rp, const float* rois, const int
     } else if (hipMemsetAsync(w.gcount, 0, sizeof(int) * N, st) != hipSuccess) {
         return check_launch("frcnn_proposal_target memset");
     }
-    const int stride = Rp + Gp;
     hipLaunchKernelGGL(pt_iou_kernel, dim3(N), dim3(1024), 0, st, rois, rcount, Rp, w.gt, w.gl,
                        w.gcount, Gp, pos_iou_thresh, neg_iou_thresh_high, neg_iou_thresh_low,
                        w.roi_all, w.assign, w.pos_list, w.neg_list, w.npos, w.nneg);
     FRCNN_LAUNCH_CHECK("pt_iou_kernel");
+    return FRCNN_OK;
+}
+
+extern "C" int frcnn_proposal_target_sample(int N, int Rp, int G, int n_sample, double pos_ratio,
+                                            const double* reg_mean, const double* reg_std,
+                                            uint32_t* rng_state, double* sample_roi, double* gt_roi_reg,
+                                            double* gt_roi_label, int32_t* sample_count, void* workspace,
+                                            size_t ws_bytes, void* stream) {
+    FRCNN_REQUIRE(N > 0 && N <= 65535 && Rp >= 0 && G >= 0 && G <= kMaxG && n_sample > 0,
+                  "frcnn_proposal_target: bad shape");
+    FRCNN_REQUIRE(rng_state && sample_roi && gt_roi_reg && gt_roi_label && sample_count && reg_mean &&
+                      reg_std,
+                  "frcnn_proposal_target: null pointer");
+    const int Gp = G > 0 ? G : 1;
+    PtWs w = carve_pt(workspace, N, Rp, Gp, n_sample);
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_proposal_target: workspace %zu < %zu",
+                  ws_bytes, w.bytes);
+    hipStream_t st = as_stream(stream);
+    const int stride = Rp + Gp;
     const int pos_per_image = static_cast<int>(std::nearbyint(n_sample * pos_ratio));  // np.round
     hipLaunchKernelGGL(pt_sample_kernel, dim3(1), dim3(kSampThreads), 0, st, N, stride, n_sample,
                        pos_per_image, w.pos_list, w.neg_list, w.npos, w.nneg, rng_state, w.sample,
@@ -1133,6 +1146,24 @@ extern "C" int frcnn_proposal_target(int N, int Rp, const float* rois, const int
                        w.spos, nrm, sample_roi, gt_roi_reg, gt_roi_label);
     FRCNN_LAUNCH_CHECK("pt_finish_kernel");
     return FRCNN_OK;
+}
+
+extern "C" int frcnn_proposal_target(int N, int Rp, const float* rois, const int32_t* rcount, int G,
+                                     const double* boxes, const double* labels, int n_sample,
+                                     double pos_ratio, double pos_iou_thresh,
+                                     double neg_iou_thresh_high, double neg_iou_thresh_low,
+                                     const double* reg_mean, const double* reg_std,
+                                     uint32_t* rng_state, double* sample_roi, double* gt_roi_reg,
+                                     double* gt_roi_label, int32_t* sample_count, void* workspace,
+                                     size_t ws_bytes, void* stream) {
+    FRCNN_REQUIRE(rng_state && sample_roi && gt_roi_reg && gt_roi_label && sample_count && reg_mean && reg_std,
+                  "frcnn_proposal_target: null pointer");
+    const int rc = frcnn_proposal_target_prepare(N, Rp, rois, rcount, G, boxes, labels, n_sample, pos_iou_thresh,
+                                                 neg_iou_thresh_high, neg_iou_thresh_low, workspace, ws_bytes,
+                                                 stream);
+    if (rc != FRCNN_OK) return rc;
+    return frcnn_proposal_target_sample(N, Rp, G, n_sample, pos_ratio, reg_mean, reg_std, rng_state, sample_roi,
+                                        gt_roi_reg, gt_roi_label, sample_count, workspace, ws_bytes, stream);
 }
 
 extern "C" int frcnn_bbox_iou(const void* a, int a_is_f64, int64_t na, const void* b, int b_is_f64,

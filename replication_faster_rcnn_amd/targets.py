@@ -156,3 +156,68 @@ def proposal_targets(rois, rcount, boxes, labels, n_sample=128, pos_ratio=0.5, p
     if own:
         rng_state_from_device(rng, st)
     return s_roi, s_reg, s_lab, s_cnt
+
+
+class ProposalTargetPlan:
+    """The RNG-free half of ProposalTargetCreator (proposal_targets_prepare):
+    gt concat, IoU, argmax and the fg / bg lists in a workspace, ready for the draws."""
+
+    def __init__(self, N, Rp, G, n_sample, ws):
+        self.N, self.Rp, self.G, self.n_sample, self.ws = N, Rp, G, n_sample, ws
+
+
+def proposal_targets_workspace(N, Rp, G, n_sample=128, device=None):
+    """A workspace for proposal_targets_prepare / _sample (caller-owned, so a
+    training loop can double-buffer plans across streams)."""
+    lib = _lib.load()
+    return torch.empty(max(int(lib.frcnn_proposal_target_workspace_size(N, Rp, G, n_sample)), 1),
+                       dtype=torch.uint8, device=device if device is not None else _lib.device())
+
+
+def proposal_targets_prepare(rois, rcount, boxes, labels, n_sample=128, pos_iou_thresh=0.5,
+                             neg_iou_thresh_high=0.5, neg_iou_thresh_low=0.0, workspace=None):
+    """First half of ``proposal_targets`` (utils/utils.py:221-246) on the current
+    stream; uses no RNG, so it can run on the proposals' stream, off the draws'."""
+    lib = _lib.load()
+    dev = _lib.device()
+    b, l = _gt(boxes, labels, dev)
+    r = rois.to(dev, torch.float32).contiguous()
+    c = rcount.to(dev, torch.int32).contiguous()
+    N, G = b.shape[:2]
+    Rp = r.size(1)
+    ws = workspace if workspace is not None else proposal_targets_workspace(N, Rp, G, n_sample, dev)
+    _lib.check(lib.frcnn_proposal_target_prepare(N, Rp, _lib.ptr(r), _lib.ptr(c), G, _lib.ptr(b), _lib.ptr(l),
+                                                 int(n_sample), float(pos_iou_thresh), float(neg_iou_thresh_high),
+                                                 float(neg_iou_thresh_low), _lib.ptr(ws), ws.numel(),
+                                                 _lib.stream_ptr()), "proposal_target_prepare")
+    return ProposalTargetPlan(N, Rp, G, int(n_sample), ws)
+
+
+def proposal_targets_sample(plan, pos_ratio=0.5, reg_normalize_mean=(0., 0., 0., 0.),
+                            reg_normalize_std=(0.1, 0.1, 0.2, 0.2), rng=None, out=None):
+    """Second half of ``proposal_targets`` (utils/utils.py:248-276): the draws
+    (numpy's global RNG, or the device stream ``rng``), sample order and
+    regression targets, on the current stream after ``plan``'s prepare (order
+    the streams with an event).  ``out`` = caller-owned (sample_roi, gt_roi_reg,
+    gt_roi_label, count) as ``proposal_targets`` returns them."""
+    lib = _lib.load()
+    dev = plan.ws.device
+    N, S = plan.N, plan.n_sample
+    if out is None:
+        out = (torch.empty((N, S, 4), dtype=torch.float64, device=dev),
+               torch.empty((N, S, 4), dtype=torch.float64, device=dev),
+               torch.empty((N, S), dtype=torch.float64, device=dev),
+               torch.empty((N,), dtype=torch.int32, device=dev))
+    s_roi, s_reg, s_lab, s_cnt = out
+    mean = np.asarray(reg_normalize_mean, np.float32).astype(np.float64)  # utils/utils.py:272
+    std = np.asarray(reg_normalize_std, np.float32).astype(np.float64)
+    own = rng is None
+    if own:
+        rng, st = rng_state_to_device(dev)
+    _lib.check(lib.frcnn_proposal_target_sample(N, plan.Rp, plan.G, S, float(pos_ratio), mean.ctypes.data,
+                                                std.ctypes.data, _lib.ptr(rng), _lib.ptr(s_roi), _lib.ptr(s_reg),
+                                                _lib.ptr(s_lab), _lib.ptr(s_cnt), _lib.ptr(plan.ws),
+                                                plan.ws.numel(), _lib.stream_ptr()), "proposal_target_sample")
+    if own:
+        rng_state_from_device(rng, st)
+    return s_roi, s_reg, s_lab, s_cnt

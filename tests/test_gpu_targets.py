@@ -258,6 +258,41 @@ def test_anchor_targets_prepare_sample_split(rng_guard):
     assert torch.equal(rng_a, rng_b)
 
 
+def test_proposal_targets_prepare_sample_split(rng_guard):
+    """proposal_targets_prepare (on a side stream) + proposal_targets_sample ==
+    the one-call proposal_targets: same samples, targets, counts and RNG stream."""
+    N, G, img = 3, 32, 600
+    r = np.random.default_rng(5)
+    rois = np.zeros((N, 300, 4), np.float32)
+    for i in range(N):
+        lo = r.uniform(0, 500, (300, 2))
+        rois[i] = np.concatenate([lo, lo + r.uniform(8, 200, (300, 2))], 1).clip(0, img)
+    rp = torch.from_numpy(rois).cuda()
+    cnt = torch.tensor([300, 120, 0], dtype=torch.int32).cuda()
+    bl = [synth.gt_boxes(img, img, G, 9, i, n_valid=[32, 5, 0][i]) for i in range(N)]
+    boxes = torch.from_numpy(np.stack([b for b, _ in bl])).cuda()
+    labels = torch.from_numpy(np.stack([l for _, l in bl])).cuda()
+    np.random.seed(23)
+    rng_a, _ = U.rng_state_to_device(torch.device("cuda"))
+    ref = [targets.proposal_targets(rp, cnt, boxes, labels, rng=rng_a) for _ in range(2)]
+    np.random.seed(23)
+    rng_b, _ = U.rng_state_to_device(torch.device("cuda"))
+    side = torch.cuda.Stream()
+    got = []
+    for _ in range(2):
+        with torch.cuda.stream(side):
+            plan = targets.proposal_targets_prepare(rp, cnt, boxes, labels)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        torch.cuda.current_stream().wait_event(ev)
+        got.append(targets.proposal_targets_sample(plan, rng=rng_b))
+    torch.cuda.synchronize()
+    for a, b in zip(ref, got):
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+    assert torch.equal(rng_a, rng_b)
+
+
 def test_cfg5_full_batch_targets(rng_guard):
     """BASELINE configs[4] at full batch: 16 images of 600x600 (38x38x9 anchors,
     32 gt slots with 1..32 valid), HIP proposals (12000 -> 600), then ONE batched
