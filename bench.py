@@ -573,21 +573,27 @@ def train_step_fn(args, c, sets, base, first_image, ev):
             pplan = targets.proposal_targets_prepare(rois, cnt, boxes, labels, n_sample=S, workspace=pt_ws[j])
             prop_ready = torch.cuda.Event()
             prop_ready.record(s_prop)
+        # the draws' stream runs only the draws (the sequential MT19937 stream);
+        # the finishing kernels go with the pool, which needs their output
         with torch.cuda.stream(s_rng):
             s_rng.wait_event(prep_ready[j])
-            reg_t, lab = targets.anchor_targets_sample(plan, rng=rng, out=at_out[j])
-            sample_ev[j].record(s_rng)
-            sample_done[j] = sample_ev[j]
+            targets.anchor_targets_draw(plan, rng=rng)
+            at_drawn = torch.cuda.Event()
+            at_drawn.record(s_rng)
             s_rng.wait_event(prop_ready)
-            s_roi, s_reg, s_lab, s_cnt = targets.proposal_targets_sample(pplan, rng=rng, out=pt_out[j])
-            pt_ev[j].record(s_rng)
-            pt_done[j] = pt_ev[j]
-            sample_rois = s_roi.float().view(-1, 4)          # train.py:86,102,107
-            ready = torch.cuda.Event()
-            ready.record(s_rng)
+            s_cnt = targets.proposal_targets_draw(pplan, rng=rng, count=pt_out[j][3])
+            pt_drawn = torch.cuda.Event()
+            pt_drawn.record(s_rng)
         with torch.cuda.stream(s_pool):
-            s_pool.wait_event(ready)
-            sample_rois.record_stream(s_pool)
+            s_pool.wait_event(at_drawn)
+            reg_t, lab = targets.anchor_targets_finish(plan, out=at_out[j])
+            sample_ev[j].record(s_pool)
+            sample_done[j] = sample_ev[j]   # at_ws[j] free for step k+2's prepare
+            s_pool.wait_event(pt_drawn)
+            s_roi, s_reg, s_lab = targets.proposal_targets_finish(pplan, s_cnt, out=pt_out[j][:3])
+            sample_rois = s_roi.float().view(-1, 4)          # train.py:86,102,107
+            pt_ev[j].record(s_pool)
+            pt_done[j] = pt_ev[j]           # pt_ws[j], pt_out[j] free for step k+2
             if timed:
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
                 e[0].record(s_pool)

@@ -231,6 +231,15 @@ int frcnn_anchor_target_prepare(int N, int A, int G, const float* anchors, const
 int frcnn_anchor_target_sample(int N, int A, int G, const float* anchors, int n_sample, double pos_ratio,
                                uint32_t* rng_state, double* reg, int32_t* label, int32_t* argmax,
                                double* max_iou, void* workspace, size_t ws_bytes, void* stream);
+/* frcnn_anchor_target_sample in two steps on the same workspace (same arguments):
+ * _draw the np.random.choice calls of utils/utils.py:190-202 (the RNG stream's only
+ * kernel), _finish the final labels and bbox2reg targets of utils/utils.py:146-150,
+ * 203-204 (any stream, after _draw: order the streams with an event). */
+int frcnn_anchor_target_draw(int N, int A, int G, int n_sample, double pos_ratio, uint32_t* rng_state,
+                             void* workspace, size_t ws_bytes, void* stream);
+int frcnn_anchor_target_finish(int N, int A, int G, const float* anchors, double* reg, int32_t* label,
+                               int32_t* argmax, double* max_iou, void* workspace, size_t ws_bytes,
+                               void* stream);
 
 /* utils/utils.py:207-276 ProposalTargetCreator.__call__, batched over N images in
  * the order of train.py:91-104.
@@ -262,6 +271,16 @@ int frcnn_proposal_target_sample(int N, int Rp, int G, int n_sample, double pos_
                                  const double* reg_mean, const double* reg_std, uint32_t* rng_state,
                                  double* sample_roi, double* gt_roi_reg, double* gt_roi_label,
                                  int32_t* sample_count, void* workspace, size_t ws_bytes, void* stream);
+/* frcnn_proposal_target_sample in two steps on the same workspace: _draw the
+ * np.random.choice calls of utils/utils.py:248-258 (sample order, sample_count),
+ * _finish sample_roi / gt_roi_reg / gt_roi_label of utils/utils.py:260-276 (any
+ * stream, after _draw). */
+int frcnn_proposal_target_draw(int N, int Rp, int G, int n_sample, double pos_ratio, uint32_t* rng_state,
+                               int32_t* sample_count, void* workspace, size_t ws_bytes, void* stream);
+int frcnn_proposal_target_finish(int N, int Rp, int G, int n_sample, const double* reg_mean,
+                                 const double* reg_std, const int32_t* sample_count, double* sample_roi,
+                                 double* gt_roi_reg, double* gt_roi_label, void* workspace, size_t ws_bytes,
+                                 void* stream);
 
 #ifdef __cplusplus
 }

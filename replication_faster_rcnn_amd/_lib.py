@@ -73,6 +73,10 @@ SIGNATURES = {
     "frcnn_proposal_target_workspace_size": (SZ, [I32, I32, I32, I32]),
     "frcnn_proposal_target": (I32, [I32, I32, P, P, I32, P, P, I32, F64, F64, F64, F64, P, P, P,
                                     P, P, P, P, P, SZ, P]),
+    "frcnn_anchor_target_draw": (I32, [I32, I32, I32, I32, F64, P, P, SZ, P]),
+    "frcnn_anchor_target_finish": (I32, [I32, I32, I32, P, P, P, P, P, P, SZ, P]),
+    "frcnn_proposal_target_draw": (I32, [I32, I32, I32, I32, F64, P, P, P, SZ, P]),
+    "frcnn_proposal_target_finish": (I32, [I32, I32, I32, I32, P, P, P, P, P, P, P, SZ, P]),
     "frcnn_proposal_target_prepare": (I32, [I32, I32, P, P, I32, P, P, I32, F64, F64, F64, P, SZ, P]),
     "frcnn_proposal_target_sample": (I32, [I32, I32, I32, I32, F64, P, P, P, P, P, P, P, P, SZ, P]),
 }

@@ -994,13 +994,10 @@ extern "C" int frcnn_anchor_target_prepare(int N, int A, int G, const float* anc
     return FRCNN_OK;
 }
 
-extern "C" int frcnn_anchor_target_sample(int N, int A, int G, const float* anchors, int n_sample,
-                                          double pos_ratio, uint32_t* rng_state, double* reg,
-                                          int32_t* label, int32_t* argmax, double* max_iou,
-                                          void* workspace, size_t ws_bytes, void* stream) {
+extern "C" int frcnn_anchor_target_draw(int N, int A, int G, int n_sample, double pos_ratio, uint32_t* rng_state,
+                                        void* workspace, size_t ws_bytes, void* stream) {
     FRCNN_REQUIRE(N > 0 && N <= 65535 && A > 0 && G >= 0 && G <= kMaxG,
                   "frcnn_anchor_target_sample: need 0 < N <= 65535, A > 0, 0 <= G <= %d", kMaxG);
-    FRCNN_REQUIRE(anchors && reg && label, "frcnn_anchor_target_sample: null pointer");
     const int n_pos_max = static_cast<int>(pos_ratio * n_sample);  // int(0.5*256) (utils/utils.py:190)
     FRCNN_REQUIRE(n_sample - (n_pos_max < 0 ? 0 : n_pos_max) <= kMaxKeep && n_pos_max <= kMaxKeep,
                   "frcnn_anchor_target_sample: n_sample too large");
@@ -1009,7 +1006,6 @@ extern "C" int frcnn_anchor_target_sample(int N, int A, int G, const float* anch
     FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_anchor_target_sample: workspace %zu < %zu",
                   ws_bytes, w.bytes);
     hipStream_t st = as_stream(stream);
-    const int nblk = (A + 255) / 256;
     if (rng_state) {
         hipLaunchKernelGGL(at_sample_kernel, dim3(1), dim3(kSampThreads), 0, st, N, A, n_sample, n_pos_max,
                            w.pos_list, w.neg_list, w.npos, w.nneg, rng_state, w.keep, w.sampled);
@@ -1017,6 +1013,21 @@ extern "C" int frcnn_anchor_target_sample(int N, int A, int G, const float* anch
     } else if (hipMemsetAsync(w.sampled, 0, sizeof(int) * 2 * N, st) != hipSuccess) {
         return check_launch("frcnn_anchor_target_sample memset");
     }
+    return FRCNN_OK;
+}
+
+extern "C" int frcnn_anchor_target_finish(int N, int A, int G, const float* anchors, double* reg, int32_t* label,
+                                          int32_t* argmax, double* max_iou, void* workspace, size_t ws_bytes,
+                                          void* stream) {
+    FRCNN_REQUIRE(N > 0 && N <= 65535 && A > 0 && G >= 0 && G <= kMaxG,
+                  "frcnn_anchor_target_sample: need 0 < N <= 65535, A > 0, 0 <= G <= %d", kMaxG);
+    FRCNN_REQUIRE(anchors && reg && label, "frcnn_anchor_target_sample: null pointer");
+    const int Gp = G > 0 ? G : 1;
+    AtWs w = carve_at(workspace, N, A, Gp);
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_anchor_target_sample: workspace %zu < %zu",
+                  ws_bytes, w.bytes);
+    hipStream_t st = as_stream(stream);
+    const int nblk = (A + 255) / 256;
     hipLaunchKernelGGL(at_finish_kernel, dim3(nblk, N), dim3(256), 0, st, anchors, A, w.gt, w.gcount,
                        Gp, w.row_arg, w.label0, w.keep, w.sampled, label, reg);
     FRCNN_LAUNCH_CHECK("at_finish_kernel");
@@ -1027,6 +1038,16 @@ extern "C" int frcnn_anchor_target_sample(int N, int A, int G, const float* anch
                                   hipMemcpyDeviceToDevice, st) != hipSuccess)
         return check_launch("frcnn_anchor_target_sample copy");
     return FRCNN_OK;
+}
+
+extern "C" int frcnn_anchor_target_sample(int N, int A, int G, const float* anchors, int n_sample,
+                                          double pos_ratio, uint32_t* rng_state, double* reg,
+                                          int32_t* label, int32_t* argmax, double* max_iou,
+                                          void* workspace, size_t ws_bytes, void* stream) {
+    FRCNN_REQUIRE(anchors && reg && label, "frcnn_anchor_target_sample: null pointer");
+    const int rc = frcnn_anchor_target_draw(N, A, G, n_sample, pos_ratio, rng_state, workspace, ws_bytes, stream);
+    if (rc != FRCNN_OK) return rc;
+    return frcnn_anchor_target_finish(N, A, G, anchors, reg, label, argmax, max_iou, workspace, ws_bytes, stream);
 }
 
 extern "C" int frcnn_anchor_target(int N, int A, int G, const float* anchors, const double* boxes,
@@ -1115,16 +1136,11 @@ extern "C" int frcnn_proposal_target_prepare(int N, int Rp, const float* rois, c
     return FRCNN_OK;
 }
 
-extern "C" int frcnn_proposal_target_sample(int N, int Rp, int G, int n_sample, double pos_ratio,
-                                            const double* reg_mean, const double* reg_std,
-                                            uint32_t* rng_state, double* sample_roi, double* gt_roi_reg,
-                                            double* gt_roi_label, int32_t* sample_count, void* workspace,
-                                            size_t ws_bytes, void* stream) {
+extern "C" int frcnn_proposal_target_draw(int N, int Rp, int G, int n_sample, double pos_ratio, uint32_t* rng_state,
+                                          int32_t* sample_count, void* workspace, size_t ws_bytes, void* stream) {
     FRCNN_REQUIRE(N > 0 && N <= 65535 && Rp >= 0 && G >= 0 && G <= kMaxG && n_sample > 0,
                   "frcnn_proposal_target: bad shape");
-    FRCNN_REQUIRE(rng_state && sample_roi && gt_roi_reg && gt_roi_label && sample_count && reg_mean &&
-                      reg_std,
-                  "frcnn_proposal_target: null pointer");
+    FRCNN_REQUIRE(rng_state && sample_count, "frcnn_proposal_target: null pointer");
     const int Gp = G > 0 ? G : 1;
     PtWs w = carve_pt(workspace, N, Rp, Gp, n_sample);
     FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_proposal_target: workspace %zu < %zu",
@@ -1136,6 +1152,23 @@ extern "C" int frcnn_proposal_target_sample(int N, int Rp, int G, int n_sample, 
                        pos_per_image, w.pos_list, w.neg_list, w.npos, w.nneg, rng_state, w.sample,
                        sample_count, w.spos);
     FRCNN_LAUNCH_CHECK("pt_sample_kernel");
+    return FRCNN_OK;
+}
+
+extern "C" int frcnn_proposal_target_finish(int N, int Rp, int G, int n_sample, const double* reg_mean,
+                                            const double* reg_std, const int32_t* sample_count,
+                                            double* sample_roi, double* gt_roi_reg, double* gt_roi_label,
+                                            void* workspace, size_t ws_bytes, void* stream) {
+    FRCNN_REQUIRE(N > 0 && N <= 65535 && Rp >= 0 && G >= 0 && G <= kMaxG && n_sample > 0,
+                  "frcnn_proposal_target: bad shape");
+    FRCNN_REQUIRE(sample_roi && gt_roi_reg && gt_roi_label && sample_count && reg_mean && reg_std,
+                  "frcnn_proposal_target: null pointer");
+    const int Gp = G > 0 ? G : 1;
+    PtWs w = carve_pt(workspace, N, Rp, Gp, n_sample);
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_proposal_target: workspace %zu < %zu",
+                  ws_bytes, w.bytes);
+    hipStream_t st = as_stream(stream);
+    const int stride = Rp + Gp;
     RegNorm nrm;
     for (int c = 0; c < 4; ++c) {
         nrm.mean[c] = reg_mean[c];
@@ -1146,6 +1179,20 @@ extern "C" int frcnn_proposal_target_sample(int N, int Rp, int G, int n_sample, 
                        w.spos, nrm, sample_roi, gt_roi_reg, gt_roi_label);
     FRCNN_LAUNCH_CHECK("pt_finish_kernel");
     return FRCNN_OK;
+}
+
+extern "C" int frcnn_proposal_target_sample(int N, int Rp, int G, int n_sample, double pos_ratio,
+                                            const double* reg_mean, const double* reg_std,
+                                            uint32_t* rng_state, double* sample_roi, double* gt_roi_reg,
+                                            double* gt_roi_label, int32_t* sample_count, void* workspace,
+                                            size_t ws_bytes, void* stream) {
+    FRCNN_REQUIRE(sample_roi && gt_roi_reg && gt_roi_label && reg_mean && reg_std,
+                  "frcnn_proposal_target: null pointer");
+    const int rc = frcnn_proposal_target_draw(N, Rp, G, n_sample, pos_ratio, rng_state, sample_count, workspace,
+                                              ws_bytes, stream);
+    if (rc != FRCNN_OK) return rc;
+    return frcnn_proposal_target_finish(N, Rp, G, n_sample, reg_mean, reg_std, sample_count, sample_roi,
+                                        gt_roi_reg, gt_roi_label, workspace, ws_bytes, stream);
 }
 
 extern "C" int frcnn_proposal_target(int N, int Rp, const float* rois, const int32_t* rcount, int G,

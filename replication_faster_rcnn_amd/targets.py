@@ -121,6 +121,38 @@ def anchor_targets_sample(plan, n_sample=256, pos_ratio=0.5, rng=None, out=None)
     return reg, lab
 
 
+def anchor_targets_draw(plan, n_sample=256, pos_ratio=0.5, rng=None):
+    """The draws of ``anchor_targets_sample`` alone (utils/utils.py:190-202), on
+    the current stream; ``anchor_targets_finish`` then writes the targets on any
+    stream ordered after it."""
+    lib = _lib.load()
+    dev = plan.ws.device
+    own = rng is None
+    if own:
+        rng, st = rng_state_to_device(dev)
+    _lib.check(lib.frcnn_anchor_target_draw(plan.N, plan.A, plan.G, int(n_sample), float(pos_ratio), _lib.ptr(rng),
+                                            _lib.ptr(plan.ws), plan.ws.numel(), _lib.stream_ptr()),
+               "anchor_target_draw")
+    if own:
+        rng_state_from_device(rng, st)
+
+
+def anchor_targets_finish(plan, out=None):
+    """Final labels and regression targets after ``anchor_targets_draw``
+    (utils/utils.py:146-150,203-204); ``out`` = caller-owned (reg, label)."""
+    lib = _lib.load()
+    dev = plan.ws.device
+    N, A = plan.N, plan.A
+    if out is None:
+        out = (torch.empty((N, A, 4), dtype=torch.float64, device=dev),
+               torch.empty((N, A), dtype=torch.int32, device=dev))
+    reg, lab = out
+    _lib.check(lib.frcnn_anchor_target_finish(N, A, plan.G, _lib.ptr(plan.anchors), _lib.ptr(reg), _lib.ptr(lab),
+                                              None, None, _lib.ptr(plan.ws), plan.ws.numel(), _lib.stream_ptr()),
+               "anchor_target_finish")
+    return reg, lab
+
+
 def proposal_targets(rois, rcount, boxes, labels, n_sample=128, pos_ratio=0.5, pos_iou_thresh=0.5,
                      neg_iou_thresh_high=0.5, neg_iou_thresh_low=0.0,
                      reg_normalize_mean=(0., 0., 0., 0.), reg_normalize_std=(0.1, 0.1, 0.2, 0.2),
@@ -221,3 +253,44 @@ def proposal_targets_sample(plan, pos_ratio=0.5, reg_normalize_mean=(0., 0., 0.,
     if own:
         rng_state_from_device(rng, st)
     return s_roi, s_reg, s_lab, s_cnt
+
+
+def proposal_targets_draw(plan, pos_ratio=0.5, rng=None, count=None):
+    """The draws of ``proposal_targets_sample`` alone (utils/utils.py:248-258:
+    sample order and per-image counts), on the current stream; returns the
+    count tensor (int32 [N], ``count`` if given)."""
+    lib = _lib.load()
+    dev = plan.ws.device
+    if count is None:
+        count = torch.empty((plan.N,), dtype=torch.int32, device=dev)
+    own = rng is None
+    if own:
+        rng, st = rng_state_to_device(dev)
+    _lib.check(lib.frcnn_proposal_target_draw(plan.N, plan.Rp, plan.G, plan.n_sample, float(pos_ratio),
+                                              _lib.ptr(rng), _lib.ptr(count), _lib.ptr(plan.ws), plan.ws.numel(),
+                                              _lib.stream_ptr()), "proposal_target_draw")
+    if own:
+        rng_state_from_device(rng, st)
+    return count
+
+
+def proposal_targets_finish(plan, count, reg_normalize_mean=(0., 0., 0., 0.),
+                            reg_normalize_std=(0.1, 0.1, 0.2, 0.2), out=None):
+    """sample_roi / gt_roi_reg / gt_roi_label after ``proposal_targets_draw``
+    (utils/utils.py:260-276), on any stream ordered after it; ``out`` =
+    caller-owned (sample_roi, gt_roi_reg, gt_roi_label)."""
+    lib = _lib.load()
+    dev = plan.ws.device
+    N, S = plan.N, plan.n_sample
+    if out is None:
+        out = (torch.empty((N, S, 4), dtype=torch.float64, device=dev),
+               torch.empty((N, S, 4), dtype=torch.float64, device=dev),
+               torch.empty((N, S), dtype=torch.float64, device=dev))
+    s_roi, s_reg, s_lab = out
+    mean = np.asarray(reg_normalize_mean, np.float32).astype(np.float64)  # utils/utils.py:272
+    std = np.asarray(reg_normalize_std, np.float32).astype(np.float64)
+    _lib.check(lib.frcnn_proposal_target_finish(N, plan.Rp, plan.G, S, mean.ctypes.data, std.ctypes.data,
+                                                _lib.ptr(count), _lib.ptr(s_roi), _lib.ptr(s_reg), _lib.ptr(s_lab),
+                                                _lib.ptr(plan.ws), plan.ws.numel(), _lib.stream_ptr()),
+               "proposal_target_finish")
+    return s_roi, s_reg, s_lab

@@ -256,6 +256,21 @@ def test_anchor_targets_prepare_sample_split(rng_guard):
         assert torch.equal(l0, l1)
         assert torch.equal(r0, r1)
     assert torch.equal(rng_a, rng_b)
+    # draws on the current stream, finish on the side stream (the bench's split)
+    np.random.seed(17)
+    rng_c, _ = U.rng_state_to_device(torch.device("cuda"))
+    for r0, l0 in ref:
+        plan = targets.anchor_targets_prepare(boxes, labels, anchors)
+        targets.anchor_targets_draw(plan, rng=rng_c)
+        ev = torch.cuda.Event()
+        ev.record()
+        with torch.cuda.stream(side):
+            side.wait_event(ev)
+            r1, l1 = targets.anchor_targets_finish(plan)
+        torch.cuda.synchronize()
+        assert torch.equal(l0, l1)
+        assert torch.equal(r0, r1)
+    assert torch.equal(rng_a, rng_c)
 
 
 def test_proposal_targets_prepare_sample_split(rng_guard):
@@ -291,6 +306,21 @@ def test_proposal_targets_prepare_sample_split(rng_guard):
         for x, y in zip(a, b):
             assert torch.equal(x, y)
     assert torch.equal(rng_a, rng_b)
+    # draws on the current stream, finish on the side stream (the bench's split)
+    np.random.seed(23)
+    rng_c, _ = U.rng_state_to_device(torch.device("cuda"))
+    for a in ref:
+        plan = targets.proposal_targets_prepare(rp, cnt, boxes, labels)
+        count = targets.proposal_targets_draw(plan, rng=rng_c)
+        ev = torch.cuda.Event()
+        ev.record()
+        with torch.cuda.stream(side):
+            side.wait_event(ev)
+            b = targets.proposal_targets_finish(plan, count)
+        torch.cuda.synchronize()
+        for x, y in zip(a, b + (count,)):
+            assert torch.equal(x, y)
+    assert torch.equal(rng_a, rng_c)
 
 
 def test_cfg5_full_batch_targets(rng_guard):
