@@ -383,12 +383,19 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
             // chunks in order, each solved exactly on the known step.
             if (wid == 0) {
                 int i_loc = i_cur, used = 0;
-                for (int c = 0; c < kWinWaves && i_loc >= 1; ++c) {
+                auto word = [&](int c) {  // chunk c's word of this lane (raw)
                     const int gc = st.off + 64 * c + lane;
                     const int bc = gc / kMtN;
-                    const uint32_t wc = mt_temper(S.ring[(st.slot + bc) % kRing][gc - bc * kMtN]);
-                    const float pa = (static_cast<float>(i_loc) + 1.0f) /
-                                     (static_cast<float>(mask_for(static_cast<uint32_t>(i_loc))) + 1.0f);
+                    return S.ring[(st.slot + bc) % kRing][gc - bc * kMtN];
+                };
+                uint32_t wn = word(0);  // the next chunk's word is read during this one's fixed point
+                for (int c = 0; c < kWinWaves && i_loc >= 1; ++c) {
+                    const uint32_t wc = mt_temper(wn);
+                    if (c + 1 < kWinWaves) wn = word(c + 1);
+                    // (a guess: any start reaches the same fixed point, so the
+                    // approximate reciprocal, not the IEEE division the build flags make '/')
+                    const float pa = (static_cast<float>(i_loc) + 1.0f) *
+                                     __builtin_amdgcn_rcpf(static_cast<float>(mask_for(static_cast<uint32_t>(i_loc))) + 1.0f);
                     const int ig0 = i_loc - static_cast<int>(static_cast<float>(lane) * pa);
                     uint64_t ac = __ballot(ig0 >= 1 && (wc & mask_for(static_cast<uint32_t>(ig0))) <=
                                                          static_cast<uint32_t>(ig0));
@@ -434,8 +441,8 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
         const int g = st.off + (wid < kWinWaves ? tid : 0);
         const int blk = g / kMtN;
         const uint32_t w = mt_temper(S.ring[(st.slot + blk) % kRing][g - blk * kMtN]);
-        const float p_acc = (static_cast<float>(i_cur) + 1.0f) /
-                            (static_cast<float>(mask_for(static_cast<uint32_t>(i_cur))) + 1.0f);
+        const float p_acc = (static_cast<float>(i_cur) + 1.0f) *
+                            __builtin_amdgcn_rcpf(static_cast<float>(mask_for(static_cast<uint32_t>(i_cur))) + 1.0f);
         auto guess = [&](int v) { return static_cast<int>(static_cast<float>(v * 64) * p_acc); };
         int base = guess(wid);
         uint64_t acc;
