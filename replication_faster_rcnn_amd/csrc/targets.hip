@@ -618,10 +618,9 @@ __device__ void fy_final(int cnt, int rec_lo, int p_lo, int p_hi, const int* J, 
 __global__ __launch_bounds__(kSampThreads) void at_sample_kernel(
     int N, int A, int n_sample, int n_pos_max, const int* __restrict__ pos_list,
     const int* __restrict__ neg_list, const int* __restrict__ npos, const int* __restrict__ nneg,
-    uint32_t* __restrict__ rng, uint8_t* __restrict__ keep, int* __restrict__ sampled) {
+    uint32_t* __restrict__ rng, int* __restrict__ sampled, int4* __restrict__ calls, int* __restrict__ jrec) {
     __shared__ WalkLds S;
     __shared__ int J[kMaxKeep];
-    __shared__ FinalLds FL;
     SPROF_T0();
     Stream st;
     stream_load(S, st, rng);
@@ -635,14 +634,19 @@ __global__ __launch_bounds__(kSampThreads) void at_sample_kernel(
             const int cnt = call == 0 ? P : Q;
             const int m = call == 0 ? n_pos_max : neg_keep;  // survivors
             const bool do_call = cnt > m;
-            if (threadIdx.x == 0) sampled[2 * n + call] = do_call ? 1 : 0;
-            if (!do_call) continue;
             const int k = cnt - m;  // disabled = perm[:k]; survivors = perm[k:]
+            if (threadIdx.x == 0) {
+                sampled[2 * n + call] = do_call ? 1 : 0;
+                calls[2 * n + call] = do_call ? make_int4(cnt, k, cnt, 0) : make_int4(0, 0, 0, 0);
+            }
+            if (!do_call) continue;
             fy_walk(S, st, cnt - 1, k, J);
             SPROF_ADD(7, cnt);
-            const int* lst = (call == 0 ? pos_list : neg_list) + static_cast<size_t>(n) * A;
-            uint8_t* kp = keep + static_cast<size_t>(n) * A;
-            fy_final(cnt, k, k, cnt, J, FL, [&](int, int v) { kp[lst[v]] = 1; });  // k >= 1
+            // the swaps of the recorded steps; the survivors are read off them by
+            // samp_emit_kernel (no RNG: off the draws' stream)
+            int* jg = jrec + static_cast<size_t>(2 * n + call) * kMaxKeep;
+            for (int i = threadIdx.x; i < cnt - k; i += kSampThreads) jg[i] = J[i];
+            __syncthreads();
         }
     }
     stream_store(S, st, rng);
@@ -772,11 +776,10 @@ __global__ __launch_bounds__(1024) void pt_iou_kernel(
 __global__ __launch_bounds__(kSampThreads) void pt_sample_kernel(
     int N, int stride, int n_sample, int pos_per_image, const int* __restrict__ pos_list,
     const int* __restrict__ neg_list, const int* __restrict__ npos, const int* __restrict__ nneg,
-    uint32_t* __restrict__ rng, int* __restrict__ sample, int* __restrict__ scount,
-    int* __restrict__ spos) {
+    uint32_t* __restrict__ rng, int* __restrict__ scount,
+    int* __restrict__ spos, int4* __restrict__ calls, int* __restrict__ jrec) {
     __shared__ WalkLds S;
     __shared__ int J[kMaxKeep];
-    __shared__ FinalLds FL;
     Stream st;
     stream_load(S, st, rng);
     __syncthreads();
@@ -785,15 +788,16 @@ __global__ __launch_bounds__(kSampThreads) void pt_sample_kernel(
         const int kp = P < pos_per_image ? P : pos_per_image;
         int kn = n_sample - kp;
         kn = Q < kn ? Q : kn;
-        int* out = sample + static_cast<size_t>(n) * n_sample;
         for (int call = 0; call < 2; ++call) {
             const int cnt = call == 0 ? P : Q;
             const int k = call == 0 ? kp : kn;
             const int off = call == 0 ? 0 : kp;
+            if (threadIdx.x == 0) calls[2 * n + call] = cnt > 0 ? make_int4(cnt, 1, k, off) : make_int4(0, 0, 0, 0);
             if (cnt == 0) continue;
             fy_walk(S, st, cnt - 1, 1, J);  // every step: J[i - 1]
-            const int* lst = (call == 0 ? pos_list : neg_list) + static_cast<size_t>(n) * stride;
-            fy_final(cnt, 1, 0, k, J, FL, [&](int p, int v) { out[off + p] = lst[v]; });
+            int* jg = jrec + static_cast<size_t>(2 * n + call) * kMaxKeep;  // read by samp_emit_kernel
+            for (int i = threadIdx.x; i < cnt - 1; i += kSampThreads) jg[i] = J[i];
+            __syncthreads();
             SPROF_ADD(8, 1);
         }
         if (threadIdx.x == 0) {
@@ -802,6 +806,38 @@ __global__ __launch_bounds__(kSampThreads) void pt_sample_kernel(
         }
     }
     stream_store(S, st, rng);
+}
+
+// One workgroup per choice() call (b = 2 image + call): the positions the
+// caller needs, read off the recorded swaps the sampler left in jrec (fy_final;
+// no RNG, so on any stream after the draws).  AnchorTarget (kMode 0) marks the
+// survivors perm[k:] in keep; ProposalTarget (1) writes the sample perm[:k] in order.
+template <int kMode>
+__global__ __launch_bounds__(kSampThreads) void samp_emit_kernel(const int4* __restrict__ calls,
+                                                                 const int* __restrict__ jrec,
+                                                                 const int* __restrict__ pos_list,
+                                                                 const int* __restrict__ neg_list, int stride,
+                                                                 uint8_t* __restrict__ keep,
+                                                                 int* __restrict__ sample, int n_sample) {
+    __shared__ int Jl[kMaxKeep];
+    __shared__ FinalLds FL;
+    const int b = blockIdx.x;
+    const int4 c = calls[b];  // cnt (0: no call), lowest recorded step, p_hi, output offset
+    if (c.x == 0) return;
+    const int cnt = c.x, rlo = c.y;
+    const int jn = cnt - rlo > 0 ? cnt - rlo : 0;
+    const int* jg = jrec + static_cast<size_t>(b) * kMaxKeep;
+    for (int i = threadIdx.x; i < jn; i += kSampThreads) Jl[i] = jg[i];
+    __syncthreads();
+    const int n = b >> 1;
+    const int* lst = ((b & 1) ? neg_list : pos_list) + static_cast<size_t>(n) * stride;
+    if (kMode == 0) {
+        uint8_t* kp = keep + static_cast<size_t>(n) * stride;
+        fy_final(cnt, rlo, rlo, cnt, Jl, FL, [&](int, int v) { kp[lst[v]] = 1; });  // rlo >= 1
+    } else {
+        int* out = sample + static_cast<size_t>(n) * n_sample + c.w;
+        fy_final(cnt, rlo, 0, c.z, Jl, FL, [&](int p, int v) { out[p] = lst[v]; });
+    }
 }
 
 // grid N x n_sample: sample_roi, normalised gt_roi_reg and gt_roi_label
@@ -927,6 +963,8 @@ struct AtWs {
     int* nneg;
     uint8_t* keep;
     int* sampled;
+    int4* calls;  // [2N] per choice() call: cnt (0: none), lowest recorded step, p_hi, offset
+    int* jrec;    // [2N][kMaxKeep] recorded swaps
     size_t bytes;
 };
 AtWs carve_at(void* ws, int N, int A, int Gp) {
@@ -947,6 +985,8 @@ AtWs carve_at(void* ws, int N, int A, int Gp) {
     w.nneg = c.take<int>(N);
     w.keep = c.take<uint8_t>(static_cast<size_t>(N) * A);
     w.sampled = c.take<int>(2 * N);
+    w.calls = c.take<int4>(2 * N);
+    w.jrec = c.take<int>(static_cast<size_t>(2 * N) * kMaxKeep);
     w.bytes = c.used();
     return w;
 }
@@ -1015,9 +1055,10 @@ extern "C" int frcnn_anchor_target_draw(int N, int A, int G, int n_sample, doubl
     hipStream_t st = as_stream(stream);
     if (rng_state) {
         hipLaunchKernelGGL(at_sample_kernel, dim3(1), dim3(kSampThreads), 0, st, N, A, n_sample, n_pos_max,
-                           w.pos_list, w.neg_list, w.npos, w.nneg, rng_state, w.keep, w.sampled);
+                           w.pos_list, w.neg_list, w.npos, w.nneg, rng_state, w.sampled, w.calls, w.jrec);
         FRCNN_LAUNCH_CHECK("at_sample_kernel");
-    } else if (hipMemsetAsync(w.sampled, 0, sizeof(int) * 2 * N, st) != hipSuccess) {
+    } else if (hipMemsetAsync(w.sampled, 0, sizeof(int) * 2 * N, st) != hipSuccess ||
+               hipMemsetAsync(w.calls, 0, sizeof(int4) * 2 * N, st) != hipSuccess) {
         return check_launch("frcnn_anchor_target_sample memset");
     }
     return FRCNN_OK;
@@ -1034,6 +1075,9 @@ extern "C" int frcnn_anchor_target_finish(int N, int A, int G, const float* anch
     FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_anchor_target_sample: workspace %zu < %zu",
                   ws_bytes, w.bytes);
     hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(samp_emit_kernel<0>, dim3(2 * N), dim3(kSampThreads), 0, st, w.calls, w.jrec, w.pos_list,
+                       w.neg_list, A, w.keep, nullptr, 0);
+    FRCNN_LAUNCH_CHECK("samp_emit_kernel");
     const int nblk = (A + 255) / 256;
     hipLaunchKernelGGL(at_finish_kernel, dim3(nblk, N), dim3(256), 0, st, anchors, A, w.gt, w.gcount,
                        Gp, w.row_arg, w.label0, w.keep, w.sampled, label, reg);
@@ -1086,6 +1130,8 @@ struct PtWs {
     int* nneg;
     int* sample;
     int* spos;
+    int4* calls;
+    int* jrec;
     size_t bytes;
 };
 PtWs carve_pt(void* ws, int N, int Rp, int Gp, int n_sample) {
@@ -1103,6 +1149,8 @@ PtWs carve_pt(void* ws, int N, int Rp, int Gp, int n_sample) {
     w.nneg = c.take<int>(N);
     w.sample = c.take<int>(static_cast<size_t>(N) * n_sample);
     w.spos = c.take<int>(N);
+    w.calls = c.take<int4>(2 * N);
+    w.jrec = c.take<int>(static_cast<size_t>(2 * N) * kMaxKeep);
     w.bytes = c.used();
     return w;
 }
@@ -1156,8 +1204,8 @@ extern "C" int frcnn_proposal_target_draw(int N, int Rp, int G, int n_sample, do
     const int stride = Rp + Gp;
     const int pos_per_image = static_cast<int>(std::nearbyint(n_sample * pos_ratio));  // np.round
     hipLaunchKernelGGL(pt_sample_kernel, dim3(1), dim3(kSampThreads), 0, st, N, stride, n_sample,
-                       pos_per_image, w.pos_list, w.neg_list, w.npos, w.nneg, rng_state, w.sample,
-                       sample_count, w.spos);
+                       pos_per_image, w.pos_list, w.neg_list, w.npos, w.nneg, rng_state, sample_count, w.spos,
+                       w.calls, w.jrec);
     FRCNN_LAUNCH_CHECK("pt_sample_kernel");
     return FRCNN_OK;
 }
@@ -1176,6 +1224,9 @@ extern "C" int frcnn_proposal_target_finish(int N, int Rp, int G, int n_sample, 
                   ws_bytes, w.bytes);
     hipStream_t st = as_stream(stream);
     const int stride = Rp + Gp;
+    hipLaunchKernelGGL(samp_emit_kernel<1>, dim3(2 * N), dim3(kSampThreads), 0, st, w.calls, w.jrec, w.pos_list,
+                       w.neg_list, stride, nullptr, w.sample, n_sample);
+    FRCNN_LAUNCH_CHECK("samp_emit_kernel");
     RegNorm nrm;
     for (int c = 0; c < 4; ++c) {
         nrm.mean[c] = reg_mean[c];
