@@ -72,6 +72,9 @@ def parse():
     ap.add_argument("--streams", type=int, default=2, choices=(1, 2),
                     help="2: the proposal layer of step k+1 runs on its own HIP stream beside "
                          "step k's RoIPool (each step still does all of its work)")
+    ap.add_argument("--rng-waits", choices=["front", "split"], default="front",
+                    help="cfg5: the draws' stream waits for both prepares before its first sampler "
+                         "(front) or for each before its sampler (split)")
     ap.add_argument("--prop-streams", type=int, default=4,
                     help="with --streams 2 (inference configs): proposal layers of consecutive "
                          "steps round-robin over this many HIP streams")
@@ -577,10 +580,13 @@ def train_step_fn(args, c, sets, base, first_image, ev):
         # the finishing kernels go with the pool, which needs their output
         with torch.cuda.stream(s_rng):
             s_rng.wait_event(prep_ready[j])
+            if args.rng_waits == "front":  # both samplers back to back (the prepares run ahead)
+                s_rng.wait_event(prop_ready)
             targets.anchor_targets_draw(plan, rng=rng)
             at_drawn = torch.cuda.Event()
             at_drawn.record(s_rng)
-            s_rng.wait_event(prop_ready)
+            if args.rng_waits != "front":
+                s_rng.wait_event(prop_ready)
             s_cnt = targets.proposal_targets_draw(pplan, rng=rng, count=pt_out[j][3])
             pt_drawn = torch.cuda.Event()
             pt_drawn.record(s_rng)
@@ -737,7 +743,7 @@ def main():
                    "parallelism": f"dp{world} (per-image sharding)", "streams": args.streams,
                    "prop_streams": args.prop_streams if (args.streams == 2 and not train) else 1,
                    "pool_on": args.pool_on if (args.streams == 2 and not train) else None,
-                   "host_io": bool(args.host_io), "roi_path": args.roi_path, "roi_cg": args.roi_cg, "roi_split": args.roi_split,
+                   "host_io": bool(args.host_io), "rng_waits": args.rng_waits, "roi_path": args.roi_path, "roi_cg": args.roi_cg, "roi_split": args.roi_split,
                    "prop_cus": args.prop_cus if (args.streams == 2 and not train) else 0,
                    "propose_path": args.propose_path,
                    "collective": (None if world == 1 else
