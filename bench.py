@@ -42,6 +42,7 @@ import os
 # Set before HIP initialises, over an environment that pins HIP's default 4
 # (FRCNN_BENCH_HW_QUEUES overrides the bench's choice).
 os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("FRCNN_BENCH_HW_QUEUES", "8")
+HW_QUEUES = int(os.environ["GPU_MAX_HW_QUEUES"])
 
 import argparse
 import json
@@ -56,8 +57,6 @@ import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-DOMINANT_KERNEL = {"infer": "roi_pool_fwd_pair_kernel<1024, 8, 7, true>",
-                   "train": "roi_pool_bwd_lead_kernel<6, 7>"}
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
@@ -148,6 +147,10 @@ def setup_dist(args):
     torch.cuda.set_device(dev_index)
     backend = None
     if world > 1:
+        # stdout carries only rank 0's JSON line: the process group's C++ log
+        # lines (gloo / RCCL) go to stderr, and so does everything of ranks > 0
+        saved = os.dup(1)
+        os.dup2(2, 1)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         shared = world > ndev  # more ranks than GPUs on this node: ranks share devices
         backend = args.dist_backend if args.dist_backend != "auto" else ("gloo" if shared else "nccl")
@@ -155,6 +158,9 @@ def setup_dist(args):
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
         else:
             dist.init_process_group("gloo")
+        if rank == 0:
+            os.dup2(saved, 1)
+        os.close(saved)
     return world, rank, dev_index, backend, ndev
 
 
@@ -441,6 +447,9 @@ def inference_step_fn(args, c, sets, base, world, n_total, backend, ev):
                 ops.propose(sc, de, img_w=c["img_w"], img_h=c["img_h"], pre_nms=c["pre_nms"],
                             post_nms=post, anchor_base=base, feat_h=c["feat_h"], feat_w=c["feat_w"],
                             out=prop_out[j])
+            if world > 1:  # the only collective: detections of all ranks, issued behind the
+                gather_after(j)  # proposals (prop_done is recorded before the pool is queued)
+            with on_prop[j]:
                 if timed:
                     e0, e1 = ev["pairs"][ev["i"]]
                     ev["i"] += 1
@@ -450,8 +459,6 @@ def inference_step_fn(args, c, sets, base, world, n_total, backend, ev):
                 if timed:
                     e1.record(s_prop)
                     ev["fwd"].append((e0, e1))
-            if world > 1:  # the only collective: detections of all ranks
-                gather_after(j)
             return cnt
         with on_prop[j]:
             if done[j] is not None:
@@ -582,6 +589,9 @@ def train_step_fn(args, c, sets, base, first_image, ev):
             s_rng.wait_event(prep_ready[j])
             if args.rng_waits == "front":  # both samplers back to back (the prepares run ahead)
                 s_rng.wait_event(prop_ready)
+            if timed:
+                d = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                d[0].record(s_rng)
             targets.anchor_targets_draw(plan, rng=rng)
             at_drawn = torch.cuda.Event()
             at_drawn.record(s_rng)
@@ -590,6 +600,9 @@ def train_step_fn(args, c, sets, base, first_image, ev):
             s_cnt = targets.proposal_targets_draw(pplan, rng=rng, count=pt_out[j][3])
             pt_drawn = torch.cuda.Event()
             pt_drawn.record(s_rng)
+            if timed:
+                d[1].record(s_rng)
+                ev["draw"].append((d[0], d[1]))
         with torch.cuda.stream(s_pool):
             s_pool.wait_event(at_drawn)
             reg_t, lab = targets.anchor_targets_finish(plan, out=at_out[j])
@@ -612,13 +625,17 @@ def train_step_fn(args, c, sets, base, first_image, ev):
                 e[2].record(s_pool)
                 ev["fwd"].append((e[0], e[1]))
                 ev["bwd"].append((e[1], e[2]))
-        state.update(s_cnt=s_cnt, lab=lab, gi=gi, am=am, bx=bx, xshape=tuple(x.shape))
+        state.update(s_cnt=s_cnt, lab=lab, reg_t=reg_t, s_roi=s_roi, s_reg=s_reg, s_lab=s_lab, pooled=pooled,
+                     gi=gi, am=am, bx=bx, xshape=tuple(x.shape))
         return s_cnt
     step.state = state
+    step.fixed = dict(rng=rng, grad=grad, boxes=boxes, labels=labels, anchors=anchors)
 
-    def alone():  # the dominant kernel (RoIPool backward) by itself, on the last step's inputs
+    def alone():  # the RoIPool backward by itself, on the last step's inputs
         ops._roi_pool_bwd(grad, state["bx"], state["am"], state["xshape"], 1.0)
     step.alone = alone
+    from replication_faster_rcnn_amd import _lib
+    step.kernel = _lib.roi_pool_bwd_kernel(N * S, N, x.size(1), x.size(2), x.size(3))
     return step
 
 
@@ -652,7 +669,7 @@ def main():
     c, sets, set_bytes = make_input_sets(cfg, mine, dev, args.input_sets)
     N = sets[0][0].size(0)
     base = A.generate_anchor_base_device(anchor_scales=c["scales"])
-    ev = {"fwd": [], "bwd": [], "i": 0,  # timing events allocated before the timed steps
+    ev = {"fwd": [], "bwd": [], "draw": [], "i": 0,  # timing events allocated before the timed steps
           "pairs": [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                     for _ in range(args.steps)]}
     if train:
@@ -719,6 +736,30 @@ def main():
                          else "roi_pool_fwd_traffic.json")
     if os.path.exists(tpath):
         traffic = json.load(open(tpath)).get(cfg, {}).get("hbm_bytes_per_launch")
+    pool_roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                 "kernel": step.kernel,
+                 "basis": "pipeline-sustained: the kernel's algorithmic bytes per step / ms_per_step "
+                          "(one launch per step)",
+                 "alg_bytes_per_launch": alg_bytes,
+                 "kernel_us_alone": alone_ms * 1e3,
+                 "frac_alone": alg_bytes / (alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                 "alone_launches": n_alone,
+                 "event_interval_us_in_pipeline": ev_ms * 1e3}
+    if train:
+        # the training step's critical path is not an HBM kernel: the target
+        # creators' draws walk numpy's sequential MT19937 stream, one workgroup
+        # each (at_sample_kernel, then pt_sample_kernel) on the draws' stream
+        draw_us = float(np.mean([a.elapsed_time(b) for a, b in ev["draw"]])) * 1e3
+        pool_roof["fwd_event_interval_us_in_pipeline"] = fwd_ms * 1e3
+        roof = {"bound": "latency", "kernel": "at_sample_kernel", "unit": "us/step",
+                "achieved": draw_us, "peak": None, "frac": None, "traffic": None,
+                "basis": "the two draws (at_sample_kernel + pt_sample_kernel, one 1024-thread workgroup "
+                         "each, sequential MT19937 stream) per step on the draws' stream, HIP events; "
+                         "latency-bound, so no HBM / MFMA peak applies",
+                "draws_share_of_step": draw_us / (ms_step * 1e3),
+                "roi_pool_bwd": pool_roof}
+        pool_roof = roof
     images = n_total * args.steps
     K = 3 * len(c["scales"])
     if train:
@@ -749,24 +790,13 @@ def main():
                    "collective": (None if world == 1 else
                                   ("RCCL all_gather_into_tensor" if backend == "nccl"
                                    else "gloo all_gather_into_tensor (ranks share a GPU)")),
-                   "devices": min(world, ndev)},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": DOMINANT_KERNEL["train"] if train else getattr(step, "kernel", DOMINANT_KERNEL["infer"]),
-                     "basis": "pipeline-sustained: the dominant kernel's algorithmic bytes per step / "
-                              "ms_per_step (one launch per step)",
-                     "alg_bytes_per_launch": alg_bytes,
-                     "kernel_us_alone": alone_ms * 1e3,
-                     "frac_alone": alg_bytes / (alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "alone_launches": n_alone,
-                     "event_interval_us_in_pipeline": ev_ms * 1e3},
+                   "devices": min(world, ndev), "hw_queues": HW_QUEUES},
+        "roofline": pool_roof,
         "cpu_baseline": None,
         "host_issue_us_per_step": t_issue / args.steps * 1e6,
     }
     if gathered:
         rec["gathered_last_step"] = gathered
-    if train:
-        rec["roofline"]["fwd_event_interval_us_in_pipeline"] = fwd_ms * 1e3
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         rec["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds, args.cpu_images, train)
         rec["cpu_baseline"]["gpu_over_cpu"] = rec["value"] / rec["cpu_baseline"]["value"]

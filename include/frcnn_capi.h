@@ -53,8 +53,10 @@ int frcnn_probe_hw_ids(uint32_t* out, int nblocks, int spin, void* stream);
 
 /* Kernel-path selection, process-global (tests and A/B tools; the default
  * "auto" is what every caller should use).  op / path:
- *   "roi_pool_fwd"   : "auto" | "wave" (image tile in LDS, one wave per RoI; RoIs grouped by
- *                      image) | "dense" (image tile, bins packed 64 per wave; any RoI order)
+ *   "roi_pool_fwd"   : "auto" | "wave" (raw image tile in LDS, compare-and-select scan, one
+ *                      wave per RoI; RoIs grouped by image; the auto choice) | "key" (ordered-key
+ *                      image tile, two-maximum scan) | "pair" (raw + pixel-pair tiles) | "dense"
+ *                      (image tile, bins packed 64 per wave; any RoI order)
  *                      | "generic" (one workgroup per RoI)
  *   "roi_pool_bwd"   : "auto" (leader-gather plane owner for 7-wide outputs, else ring) | "ring" (latency-hidden plane owner) | "plain"
  *   "propose"        : "auto" | "hybrid" | "lazy" (fused per image) | "wide" (chip-wide bitmask)
@@ -185,7 +187,11 @@ size_t frcnn_roi_pool_bwd_workspace_size(int64_t R, int N, int PH, int PW);
 int frcnn_roi_pool_bwd(const float* grad, const float* rois, const int32_t* argmax, int64_t R,
                        int N, int C, int H, int W, int PH, int PW, float spatial_scale,
                        float* grad_in, void* workspace, size_t ws_bytes, void* stream);
-
+/* The RoIPool backward kernel frcnn_roi_pool_bwd launches for this shape under
+ * the current frcnn_set_path choice (e.g. "roi_pool_bwd_lead_kernel<6, 7>"),
+ * NUL-terminated in name[len] (bench.py's label for it; the fused prep + lists
+ * launch before it is not named). */
+int frcnn_roi_pool_bwd_kernel(int64_t R, int N, int C, int H, int W, int PH, int PW, char* name, size_t len);
 
 /* --------------------------------------------------------- target creators */
 

@@ -44,6 +44,7 @@ SIGNATURES = {
     "frcnn_device_cu_count": (I32, [P]),
     "frcnn_set_path": (I32, [ctypes.c_char_p, ctypes.c_char_p]),
     "frcnn_roi_pool_fwd_kernel": (I32, [I64, I32, I32, I32, I32, I32, I32, I32, I32, P, ctypes.c_char_p, SZ]),
+    "frcnn_roi_pool_bwd_kernel": (I32, [I64, I32, I32, I32, I32, I32, I32, ctypes.c_char_p, SZ]),
     "frcnn_stream_create": (I32, [P, I32, P]),
     "frcnn_stream_destroy": (I32, [P]),
     "frcnn_stream_cu_count": (I32, [P, P]),
@@ -84,6 +85,7 @@ SIGNATURES = {
 # diagnostic entry points of instrumented builds only (not in include/frcnn_capi.h)
 DEBUG_SIGNATURES = {
     "frcnn_debug_sampler_prof": (I32, [P, I32]),  # -DFRCNN_SAMPLER_PROF (tools/probe_sampler.py)
+    "frcnn_debug_key_prof": (I32, [P, I32]),      # -DFRCNN_KEY_PROF (tools/dbg/key_prof.py)
 }
 
 _lib = None
@@ -224,6 +226,16 @@ def roi_pool_fwd_kernel(R, N, C, H, W, PH=7, PW=7, rois_sorted=True, head=True, 
     check(lib.frcnn_roi_pool_fwd_kernel(int(R), int(N), int(C), int(H), int(W), int(PH), int(PW),
                                         int(bool(rois_sorted)), int(bool(head)),
                                         ctypes.c_void_p(s.cuda_stream), buf, 128), "roi_pool_fwd_kernel")
+    return buf.value.decode()
+
+
+def roi_pool_bwd_kernel(R, N, C, H, W, PH=7, PW=7) -> str:
+    """frcnn_roi_pool_bwd_kernel: the template name of the RoIPool backward kernel
+    a call of this shape launches."""
+    lib = load()
+    buf = ctypes.create_string_buffer(128)
+    check(lib.frcnn_roi_pool_bwd_kernel(int(R), int(N), int(C), int(H), int(W), int(PH), int(PW), buf, 128),
+          "roi_pool_bwd_kernel")
     return buf.value.decode()
 
 

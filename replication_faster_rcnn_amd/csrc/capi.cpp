@@ -67,10 +67,12 @@ extern "C" int frcnn_set_path(const char* op, const char* path) {
     auto is = [&](const char* a, const char* b) { return std::strcmp(a, b) == 0; };
     const bool aut = is(path, "auto");
     if (is(op, "roi_pool_fwd") &&
-        (aut || is(path, "pair") || is(path, "wave") || is(path, "dense") || is(path, "generic"))) {
+        (aut || is(path, "pair") || is(path, "wave") || is(path, "key") || is(path, "dense") ||
+         is(path, "generic"))) {
         g_path.roi_fwd = aut ? kPathAuto : is(path, "generic") ? kPathGeneric
                                        : is(path, "dense")     ? kPathDense
                                        : is(path, "pair")      ? kPathPair
+                                       : is(path, "key")       ? kPathKey
                                                                : kPathWave;
     } else if (is(op, "roi_pool_bwd") &&
                (aut || is(path, "ring") || is(path, "plain"))) {

@@ -987,6 +987,304 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_pair_kernel(
     }
 }
 
+// ------------------------------------------------- ordered-key forward
+// pool_key: a bijection of the fp32 bit patterns onto u32 that orders the
+// non-NaN floats like '<' (sign-magnitude -> offset binary), plus one, so that
+// -0.0 (key 0x80000000) and +0.0 (0x80000001) fall into the same key class
+// (keys equal above the low kKeyBits bits).  NaN / -inf / -FLT_MAX are never
+// selected by torchvision's strict '>' against -FLT_MAX; a workgroup whose
+// planes hold any of them takes the exact scan (key_exact) for all its RoIs.
+#ifdef FRCNN_KEY_PROF
+__device__ unsigned long long g_key_prof[4];  // fast RoI-waves, re-scanning waves, re-scanned lanes, exact RoI-waves
+#define KPROF(i, v) do { if (lane == 0) atomicAdd(&g_key_prof[i], static_cast<unsigned long long>(v)); } while (0)
+#else
+#define KPROF(i, v) do {} while (0)
+#endif
+#ifndef FRCNN_KEY_DBG
+#define FRCNN_KEY_DBG 0  // experiment builds only: 1 no check, 2 no K pass, 4 no stores
+#endif
+constexpr int kKeyBits = 10;
+constexpr uint32_t kKeyMask = (1u << kKeyBits) - 1;
+constexpr uint32_t kKeyZero = 0x80000001u;  // pool_key(+0.0f): the empty-window sentinel
+
+__device__ __forceinline__ uint32_t pool_key(float v) {
+    const uint32_t u = __float_as_uint(v);
+    return (u ^ (static_cast<uint32_t>(static_cast<int32_t>(u) >> 31) | 0x80000000u)) + 1u;
+}
+__device__ __forceinline__ uint32_t pool_unkey(uint32_t k) {
+    const uint32_t u = k - 1u;
+    return u ^ (~static_cast<uint32_t>(static_cast<int32_t>(u) >> 31) | 0x80000000u);
+}
+
+// torchvision's exact window scan (strict '>' from -FLT_MAX, row-major first
+// maximum, empty window -> 0 / -1) over the key tile, CG channels at once.
+template <int NP>
+__device__ __forceinline__ void key_exact(const uint4* __restrict__ k4, int p0, int hh, int ww, int W,
+                                          float (&mv)[4 * NP], int (&mi)[4 * NP]) {
+    const float init = (hh <= 0 || ww <= 0) ? 0.0f : -FLT_MAX;
+#pragma unroll
+    for (int c = 0; c < 4 * NP; ++c) {
+        mv[c] = init;
+        mi[c] = -1;
+    }
+    for (int dh = 0; dh < hh; ++dh) {
+        for (int dw = 0; dw < ww; ++dw) {
+            const int p = p0 + dh * W + dw;
+            const uint4* pp = reinterpret_cast<const uint4*>(tile_px<NP>(reinterpret_cast<const float4*>(k4), p));
+#pragma unroll
+            for (int q = 0; q < NP; ++q) {
+                const uint4 t = pp[16 * q];
+                const uint32_t tt[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float v = __uint_as_float(pool_unkey(tt[j]));
+                    if (v > mv[4 * q + j]) {
+                        mv[4 * q + j] = v;
+                        mi[4 * q + j] = p;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// The default forward for RoIs grouped by image.  Grid, RoI shares, the LDS
+// RoI counter and the per-chunk geometry are the wave kernel's (one wave per
+// RoI, lane = bin, CG channels per lane); the tile holds pool_key(x) instead of
+// x, and the scan replaces torchvision's compare + two selects per
+// pixel-channel with two u32 maxima and one and-or:
+//   M = max over the window of key           (the maximum, exactly)
+//   K = max over the window of (key & ~mask) | (mask - (p - p0))
+// K's class is M's class, and among the window's pixels of that class K names
+// the first in row-major order (p - p0 grows with it).  If that pixel's value
+// is M, it is the first pixel holding the maximum: torchvision's answer, and
+// the output value is pool_unkey(M) (bit-exact incl. the sign of a zero).  The
+// check reads the named pixel's key from the tile; a lane whose check fails
+// for any channel (another value of the same class precedes the maximum, e.g.
+// -0.0 before +0.0: rare) re-scans its window exactly.
+// Loops are wave-uniform over the RoI's largest bin (hmax x wmax, from the
+// chunk prologue), each lane's pixel clamped into its own window (re-reading a
+// pixel changes neither maximum), two pixels per step (v_max3_u32).
+template <int NT, int CG, int FIX, bool HEAD>
+__global__ __launch_bounds__(NT) void roi_pool_fwd_key_kernel(
+    const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W, int PH_, int PW_,
+    float ss, float* __restrict__ out, int32_t* __restrict__ argmax, int geo_cap, HeadArgs hd) {
+    const int PH = FIX ? FIX : PH_, PW = FIX ? FIX : PW_;
+    constexpr int NP = CG / 4;
+    extern __shared__ __attribute__((aligned(16))) uint4 k4[];  // key tile (tile_px layout); geometry after
+    __shared__ int s_red[2 * (NT / 64)];
+    __shared__ int s_next;
+    const int b = blockIdx.z;
+    const int c0 = blockIdx.x * CG;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int HW = H * W;
+    const int HWs = (HW + 16) & ~15;  // + the zero sentinel pixel HW
+    const int PHW = PH * PW;
+    const int split = gridDim.y, z = blockIdx.y;
+    const int N = gridDim.z - 1;
+    PPROF_T(0);
+    if (b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
+        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, 0, N, s_red, 1)
+                             : roi_range_sorted<NT>(rois, R, 0, N, s_red);
+        const int n_lo = rg.x, tot = n_lo + (R - rg.y);
+        const int lo = static_cast<int>(static_cast<int64_t>(tot) * z / split);
+        const int hi = static_cast<int>(static_cast<int64_t>(tot) * (z + 1) / split);
+        if (HEAD && hd.boxes && blockIdx.x == 0)
+            for (int t = lo + tid; t < hi; t += NT) {
+                const int r = t < n_lo ? t : rg.y + (t - n_lo);
+                float bx[5];
+                head_box(rois, hd, r, bx);
+#pragma unroll
+                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
+            }
+        for (int e = lo * CG * PHW + tid; e < hi * CG * PHW; e += NT) {
+            const int t = e / (CG * PHW);
+            const int rem = e - t * (CG * PHW);
+            const int r = t < n_lo ? t : rg.y + (t - n_lo);
+            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + rem;
+            out[o] = 0.0f;
+            argmax[o] = -1;
+        }
+        return;
+    }
+    const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, b, b + 1, s_red, 1)
+                         : roi_range_sorted<NT>(rois, R, b, b + 1, s_red);
+    const int rbase = rg.x, nr = rg.y - rg.x;
+    PPROF_T(1);
+    if (z >= nr) return;
+    const int nmine = (nr - z + split - 1) / split;  // items z, z+split, ...
+    PPROF_ROIS(nmine);
+    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
+    const float4* t4 = reinterpret_cast<const float4*>(k4);
+    if (tid < NP) {
+        uint4* s = const_cast<uint4*>(reinterpret_cast<const uint4*>(tile_px<NP>(t4, HW)));
+        s[16 * tid] = make_uint4(kKeyZero, kKeyZero, kKeyZero, kKeyZero);
+    }
+    int special = 0;
+    for (int p = tid; p < HW; p += NT) {
+        uint32_t v[CG];
+#pragma unroll
+        for (int q = 0; q < CG; ++q) {
+            const float e = src[static_cast<size_t>(q) * HW + p];
+            special |= !(e > -FLT_MAX);  // NaN, -inf, -FLT_MAX
+            v[q] = pool_key(e);
+        }
+        uint4* pp = const_cast<uint4*>(reinterpret_cast<const uint4*>(tile_px<NP>(t4, p)));
+#pragma unroll
+        for (int k = 0; k < NP; ++k) pp[16 * k] = make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    }
+    special = __syncthreads_or(special);
+    int4* s_geo = reinterpret_cast<int4*>(k4 + NP * HWs);
+    int* s_ext = reinterpret_cast<int*>(s_geo + geo_cap);  // hmax | wmax << 16
+    const int ph = lane / PW, pw = lane - (lane / PW) * PW;
+    const bool act = lane < PHW;
+    for (int k0 = 0; k0 < nmine; k0 += geo_cap) {
+        const int cn = min(geo_cap, nmine - k0);
+        for (int i = tid; i < cn; i += NT) {
+            const int r = rbase + z + (k0 + i) * split;
+            float bx[5];
+            if (HEAD) {
+                head_box(rois, hd, r, bx);
+                if (hd.boxes && blockIdx.x == 0) {
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 5; ++j) bx[j] = rois[static_cast<size_t>(r) * 5 + j];
+            }
+            const RoiGeom gm = roi_geom(bx, ss, PH, PW);
+            int hm = 1, wm = 1;
+            for (int t = 0; t < PH; ++t) {
+                const int4 gb = geom_bin(gm, H, W, t, 0);
+                hm = max(hm, gb.y - gb.x);
+            }
+            for (int t = 0; t < PW; ++t) {
+                const int4 gb = geom_bin(gm, H, W, 0, t);
+                wm = max(wm, gb.w - gb.z);
+            }
+            s_geo[i] = make_int4(gm.sh, gm.sw, __float_as_int(gm.bh), __float_as_int(gm.bw));
+            s_ext[i] = hm | (wm << 16);
+        }
+        if (tid == 0) s_next = 0;
+        __syncthreads();
+        if (k0 == 0) PPROF_T(2);
+        int k = 0;
+        if (lane == 0) k = atomicAdd(&s_next, 1);
+        k = __builtin_amdgcn_readfirstlane(k);
+        while (k < cn) {
+            int kn = 0;
+            if (lane == 0) kn = atomicAdd(&s_next, 1);  // prefetch the next item
+            const int r = rbase + z + (k0 + k) * split;
+            const int4 gq = s_geo[k];
+            const int ex = __builtin_amdgcn_readfirstlane(s_ext[k]);
+            const int hmax = ex & 0xFFFF, wmax = ex >> 16;
+            RoiGeom gm;
+            gm.sh = gq.x;
+            gm.sw = gq.y;
+            gm.bh = __int_as_float(gq.z);
+            gm.bw = __int_as_float(gq.w);
+            int4 g = geom_bin(gm, H, W, ph, pw);
+            if (!act) g = make_int4(0, 0, 0, 0);
+            const bool empty = g.y <= g.x || g.w <= g.z;
+            const int p0 = empty ? HW : g.x * W + g.z;
+            float val[CG];
+            int idx[CG];
+            if (special || (hmax - 1) * W + (wmax - 1) > static_cast<int>(kKeyMask)) {
+                KPROF(3, 1);
+                key_exact<NP>(k4, p0, empty ? 0 : g.y - g.x, empty ? 0 : g.w - g.z, W, val, idx);
+            } else {
+                KPROF(0, 1);
+                const int hh1 = empty ? 0 : g.y - g.x - 1, ww1 = empty ? 0 : g.w - g.z - 1;
+                const uint32_t cb = static_cast<uint32_t>(p0) + kKeyMask;
+                uint32_t K[CG], M[CG];
+#pragma unroll
+                for (int c = 0; c < CG; ++c) K[c] = M[c] = 0u;
+                for (int dh = 0; dh < hmax; ++dh) {
+                    const int rb = p0 + min(dh, hh1) * W;
+                    int dw = 0;
+                    for (; dw + 1 < wmax; dw += 2) {  // two pixels per step
+                        const int pa = rb + min(dw, ww1), pb = rb + min(dw + 1, ww1);
+                        const uint4* qa = reinterpret_cast<const uint4*>(tile_px<NP>(t4, pa));
+                        const uint4* qb = reinterpret_cast<const uint4*>(tile_px<NP>(t4, pb));
+                        uint4 va[NP], vb[NP];
+#pragma unroll
+                        for (int q = 0; q < NP; ++q) {
+                            va[q] = qa[16 * q];
+                            vb[q] = qb[16 * q];
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                        const uint32_t ca = cb - static_cast<uint32_t>(pa), cc = cb - static_cast<uint32_t>(pb);
+#pragma unroll
+                        for (int q = 0; q < NP; ++q) {
+                            const uint32_t ta[4] = {va[q].x, va[q].y, va[q].z, va[q].w};
+                            const uint32_t tb[4] = {vb[q].x, vb[q].y, vb[q].z, vb[q].w};
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                const uint32_t ka = (ta[j] & ~kKeyMask) | ca, kb = (tb[j] & ~kKeyMask) | cc;
+                                if (!(FRCNN_KEY_DBG & 2)) K[4 * q + j] = max(K[4 * q + j], max(ka, kb));
+                                M[4 * q + j] = max(M[4 * q + j], max(ta[j], tb[j]));
+                            }
+                        }
+                    }
+                    if (dw < wmax) {  // odd width: the last column alone
+                        const int pa = rb + min(dw, ww1);
+                        const uint4* qa = reinterpret_cast<const uint4*>(tile_px<NP>(t4, pa));
+                        uint4 va[NP];
+#pragma unroll
+                        for (int q = 0; q < NP; ++q) va[q] = qa[16 * q];
+                        __builtin_amdgcn_sched_barrier(0);
+                        const uint32_t ca = cb - static_cast<uint32_t>(pa);
+#pragma unroll
+                        for (int q = 0; q < NP; ++q) {
+                            const uint32_t ta[4] = {va[q].x, va[q].y, va[q].z, va[q].w};
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                if (!(FRCNN_KEY_DBG & 2)) K[4 * q + j] = max(K[4 * q + j], (ta[j] & ~kKeyMask) | ca);
+                                M[4 * q + j] = max(M[4 * q + j], ta[j]);
+                            }
+                        }
+                    }
+                }
+                // the first pixel of the maximum's class and the check of its key
+                // against the maximum (LDS: a reload from memory would wait, in
+                // vmcnt order, for the previous RoI's stores); an empty window
+                // names the sentinel pixel (key +0.0 = its maximum) and argmax -1
+                const int ioff = empty ? -(HW + 1) : 0;
+                uint32_t bad = 0;
+#pragma unroll
+                for (int c = 0; c < CG; ++c) {
+                    const int p = static_cast<int>(cb - (K[c] & kKeyMask));
+                    idx[c] = p + ioff;
+                    if (!(FRCNN_KEY_DBG & 1)) {
+                        const uint32_t t = reinterpret_cast<const uint32_t*>(tile_px<NP>(t4, p))[64 * (c / 4) + (c % 4)];
+                        bad |= t ^ M[c];
+                    }
+                    val[c] = __uint_as_float(pool_unkey(M[c]));
+                }
+                if (__builtin_amdgcn_ballot_w64(bad != 0)) {
+                    KPROF(1, 1);
+                    KPROF(2, __builtin_popcountll(__builtin_amdgcn_ballot_w64(bad != 0)));
+                    if (bad) key_exact<NP>(k4, p0, empty ? 0 : g.y - g.x, empty ? 0 : g.w - g.z, W, val, idx);
+                }
+            }
+            if (act && !(FRCNN_KEY_DBG & 4)) {
+                const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
+                float* op = out + o;
+                int32_t* ap = argmax + o;
+#pragma unroll
+                for (int c = 0; c < CG; ++c) {
+                    op[c * PHW] = val[c];
+                    ap[c * PHW] = idx[c];
+                }
+            }
+            k = __builtin_amdgcn_readfirstlane(kn);
+        }
+        __syncthreads();  // the chunk's geometry and s_next are reused
+    }
+    PPROF_T(3);
+}
+
 // nets/heads.py:42-47 (fp32 divide, then multiply) + [idx, box] pack.
 __global__ __launch_bounds__(256) void roi_transform_kernel(const float* __restrict__ rois,
                                                             const float* __restrict__ inds,
@@ -1741,6 +2039,16 @@ extern "C" int frcnn_debug_bwd_prof(unsigned long long* out, int reset) {
     return 0;
 }
 #endif
+#ifdef FRCNN_KEY_PROF
+extern "C" int frcnn_debug_key_prof(unsigned long long* out, int reset) {
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_key_prof), sizeof(g_key_prof));
+    if (reset) {
+        unsigned long long z[4] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_key_prof), z, sizeof(z));
+    }
+    return 0;
+}
+#endif
 #ifdef FRCNN_POOL_PROF
 extern "C" int frcnn_debug_pool_prof(unsigned long long* times, unsigned* rois, int reset) {
     (void)hipMemcpyFromSymbol(times, HIP_SYMBOL(g_pool_prof), sizeof(g_pool_prof));
@@ -1779,12 +2087,12 @@ struct PxPlan {
     int cg = 0, geo_cap = 0, split = 1;
     size_t lds = 0;
 };
-PxPlan px_plan(int C, int N, int H, int W, int PHW, hipStream_t st) {
+PxPlan px_plan(int C, int N, int H, int W, int PHW, hipStream_t st, size_t per_geo = sizeof(int4)) {
     PxPlan pl;
     const size_t HW = static_cast<size_t>(H) * W;
     if (N <= 0 || HW == 0 || PHW > 64 || H > 65535 || W > 65535) return pl;
     constexpr size_t kReserve = 1024;  // static LDS + allocation rounding
-    constexpr size_t kMinGeo = 64 * sizeof(int4);
+    const size_t kMinGeo = 64 * per_geo;
     const size_t HWs = (HW + 16) & ~static_cast<size_t>(15);  // + the zero sentinel pixel
     for (int cg : {16, 8, 4}) {
         if (C % cg != 0) continue;
@@ -1794,10 +2102,10 @@ PxPlan px_plan(int C, int N, int H, int W, int PHW, hipStream_t st) {
         if (2 * (tile + kMinGeo + kReserve) <= kLdsPerCu) per_cu = 2;
         else if (tile + kMinGeo + kReserve <= kLdsPerCu) per_cu = 1;
         if (!per_cu) continue;
-        const size_t geo = (kLdsPerCu / per_cu - kReserve - tile) / sizeof(int4);
+        const size_t geo = (kLdsPerCu / per_cu - kReserve - tile) / per_geo;
         pl.geo_cap = static_cast<int>(geo > 512 ? 512 : geo);
         pl.cg = cg;
-        pl.lds = tile + static_cast<size_t>(pl.geo_cap) * sizeof(int4);
+        pl.lds = tile + static_cast<size_t>(pl.geo_cap) * per_geo;
         const int64_t wgs = static_cast<int64_t>(C / cg) * N;
         int64_t sp = (static_cast<int64_t>(stream_cu_count(st)) * per_cu + wgs - 1) / wgs;
         if (path_cfg().roi_split > 0) sp = path_cfg().roi_split;  // A/B override
@@ -1824,6 +2132,31 @@ int px_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, in
     }
 #undef FRCNN_PX
     FRCNN_LAUNCH_CHECK("roi_pool_fwd_wave_kernel");
+    return FRCNN_OK;
+}
+
+// The ordered-key forward: the wave kernel's plan with 20 B of geometry per RoI.
+PxPlan key_plan(int C, int N, int H, int W, int PHW, hipStream_t st) {
+    return px_plan(C, N, H, W, PHW, st, sizeof(int4) + sizeof(int));
+}
+
+template <bool HEAD>
+int key_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
+               int PH, int PW, float ss, float* out, int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
+    const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(pl.split), static_cast<unsigned>(N + 1));
+    const bool fix7 = PH == 7 && PW == 7;
+#define FRCNN_KEY(CG, FX)                                                                                  \
+    hipLaunchKernelGGL((roi_pool_fwd_key_kernel<1024, CG, FX, HEAD>), grid, dim3(1024), pl.lds, st, x, rois, \
+                       static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd)
+    if (pl.cg == 16) {
+        if (fix7) FRCNN_KEY(16, 7); else FRCNN_KEY(16, 0);
+    } else if (pl.cg == 8) {
+        if (fix7) FRCNN_KEY(8, 7); else FRCNN_KEY(8, 0);
+    } else {
+        if (fix7) FRCNN_KEY(4, 7); else FRCNN_KEY(4, 0);
+    }
+#undef FRCNN_KEY
+    FRCNN_LAUNCH_CHECK("roi_pool_fwd_key_kernel");
     return FRCNN_OK;
 }
 
@@ -1943,6 +2276,56 @@ int dense_launch(const DensePlan& pl, const float* x, const float* rois, const i
     FRCNN_LAUNCH_CHECK("roi_pool_fwd_dense_kernel");
     return FRCNN_OK;
 }
+// One launch-plan choice for frcnn_roi_pool_fwd, frcnn_roi_pool_fwd_head and
+// the kernel-name query, so the name a caller records is the kernel launched.
+enum FwdKind { kFwdPair, kFwdKey, kFwdWave, kFwdDense, kFwdDenseList, kFwdGeneric };
+struct FwdChoice {
+    int kind = kFwdGeneric;
+    PxPlan px;
+    DensePlan dn;
+};
+FwdChoice choose_fwd(int N, int C, int H, int W, int PH, int PW, bool sorted, hipStream_t st) {
+    FwdChoice ch;
+    const int path = path_cfg().roi_fwd;
+    const int PHW = PH * PW;
+    if (sorted && C > 0) {
+        // the pair-tile kernel only on request: alone it matched the wave kernel,
+        // beside other steps' kernels it lost (profiles/r3_experiments.md)
+        if (path == kPathPair && (ch.px = pair_plan(C, N, H, W, PHW, st)).cg) {
+            ch.kind = kFwdPair;
+            return ch;
+        }
+        if (path == kPathKey && (ch.px = key_plan(C, N, H, W, PHW, st)).cg) {
+            ch.kind = kFwdKey;
+            return ch;
+        }
+        if ((path == kPathAuto || path == kPathWave || path == kPathPair || path == kPathKey) &&
+            (ch.px = px_plan(C, N, H, W, PHW, st)).cg) {
+            ch.kind = kFwdWave;
+            return ch;
+        }
+    }
+    ch.px = PxPlan{};
+    if (path != kPathGeneric && C > 0 && (ch.dn = dense_plan(C, N, H, W, PHW)).cg) {
+        ch.kind = sorted ? kFwdDense : kFwdDenseList;
+        return ch;
+    }
+    ch.kind = kFwdGeneric;
+    return ch;
+}
+
+template <bool HEAD>
+int fwd_tile_launch(const FwdChoice& ch, const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
+                    int PH, int PW, float ss, float* out, int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
+    switch (ch.kind) {
+        case kFwdPair: return pair_launch<HEAD>(ch.px, x, rois, R, N, C, H, W, PH, PW, ss, out, argmax, hd, st);
+        case kFwdKey: return key_launch<HEAD>(ch.px, x, rois, R, N, C, H, W, PH, PW, ss, out, argmax, hd, st);
+        case kFwdWave: return px_launch<HEAD>(ch.px, x, rois, R, N, C, H, W, PH, PW, ss, out, argmax, hd, st);
+        default:
+            return dense_launch<HEAD, false>(ch.dn, x, rois, nullptr, nullptr, R, N, C, H, W, PH, PW, ss, out,
+                                             argmax, hd, st);
+    }
+}
 }  // namespace
 
 extern "C" size_t frcnn_roi_pool_fwd_workspace_size(int64_t R, int N, int C) {
@@ -1961,30 +2344,15 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
     if (R == 0 || C == 0) return FRCNN_OK;
     FRCNN_REQUIRE(x && rois && out && argmax, "frcnn_roi_pool_fwd: null pointer");
     hipStream_t st = as_stream(stream);
-    const int path = path_cfg().roi_fwd;
-    // the pair-tile kernel only on request: alone it matches the wave kernel
-    // (64.9-70.1 vs 67.1-69.2 us at cfg2), beside other steps' kernels it loses
-    // (cfg2 bench 88.8-91.1k vs 94.4-97.6k images/s, cfg1 9.4k vs 10.1k)
-    const PxPlan pp = (rois_sorted && path == kPathPair) ? pair_plan(C, N, H, W, PH * PW, st) : PxPlan{};
-    if (pp.cg)
-        return pair_launch<false>(pp, x, rois, R, N, C, H, W, PH, PW, spatial_scale, out, argmax, HeadArgs{}, st);
-    const PxPlan xp = (rois_sorted && (path == kPathAuto || path == kPathWave || path == kPathPair))
-                          ? px_plan(C, N, H, W, PH * PW, st)
-                          : PxPlan{};
-    if (xp.cg)
-        return px_launch<false>(xp, x, rois, R, N, C, H, W, PH, PW, spatial_scale, out, argmax, HeadArgs{}, st);
-    const DensePlan pl = path == kPathGeneric ? DensePlan{} : dense_plan(C, N, H, W, PH * PW);
-    if (pl.cg && rois_sorted)
-        return dense_launch<false, false>(pl, x, rois, nullptr, nullptr, R, N, C, H, W, PH, PW,
-                                          spatial_scale, out, argmax, HeadArgs{}, st);
-    if (pl.cg) {  // any RoI order: per-image lists first
+    const FwdChoice ch = choose_fwd(N, C, H, W, PH, PW, rois_sorted != 0, st);
+    if (ch.kind == kFwdDenseList) {  // any RoI order: per-image lists first
         FwdWs w = carve_fwd(workspace, R, N);
         FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_fwd: workspace %zu < %zu",
                       ws_bytes, w.bytes);
         hipLaunchKernelGGL(roi_lists_kernel, dim3(N + 1), dim3(1024), 0, st, rois, static_cast<int>(R), N,
                            w.list, w.cnt);
         FRCNN_LAUNCH_CHECK("roi_lists_kernel");
-        int rc = dense_launch<false, true>(pl, x, rois, w.list, w.cnt, R, N, C, H, W, PH, PW, spatial_scale,
+        int rc = dense_launch<false, true>(ch.dn, x, rois, w.list, w.cnt, R, N, C, H, W, PH, PW, spatial_scale,
                                            out, argmax, HeadArgs{}, st);
         if (rc) return rc;
         hipLaunchKernelGGL(roi_pool_invalid_fill_kernel, dim3(64), dim3(256), 0, st, w.list, w.cnt,
@@ -1992,6 +2360,8 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
         FRCNN_LAUNCH_CHECK("roi_pool_invalid_fill_kernel");
         return FRCNN_OK;
     }
+    if (ch.kind != kFwdGeneric)
+        return fwd_tile_launch<false>(ch, x, rois, R, N, C, H, W, PH, PW, spatial_scale, out, argmax, HeadArgs{}, st);
     // generic path: one workgroup per RoI, gathers from L1/L2
     const size_t total = static_cast<size_t>(C) * PH * PW;
     const bool aligned = (reinterpret_cast<uintptr_t>(out) % 16 == 0) &&
@@ -2006,32 +2376,32 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
     return FRCNN_OK;
 }
 
+// head != 0 names the launch of frcnn_roi_pool_fwd_head for 16-B aligned [R,4]
+// rois (every torch allocation); unaligned rois take the transform + the
+// head == 0 launch.
 extern "C" int frcnn_roi_pool_fwd_kernel(int64_t R, int N, int C, int H, int W, int PH, int PW, int rois_sorted,
                                          int head, void* stream, char* name, size_t len) {
     FRCNN_REQUIRE(name && len > 0, "frcnn_roi_pool_fwd_kernel: null name");
     FRCNN_REQUIRE(R >= 0 && N >= 0 && C >= 0 && H >= 0 && W >= 0 && PH > 0 && PW > 0,
                   "frcnn_roi_pool_fwd_kernel: bad shape");
-    hipStream_t st = as_stream(stream);
-    const int path = path_cfg().roi_fwd;
+    const FwdChoice ch = choose_fwd(N, C, H, W, PH, PW, rois_sorted != 0, as_stream(stream));
     const int fx = PH == 7 && PW == 7 ? 7 : 0;
     const char* hb = head ? "true" : "false";
-    const bool ok = rois_sorted && C > 0;
-    const PxPlan pp = (ok && path == kPathPair) ? pair_plan(C, N, H, W, PH * PW, st) : PxPlan{};
-    const PxPlan xp = (!pp.cg && ok && (path == kPathAuto || path == kPathWave || path == kPathPair))
-                          ? px_plan(C, N, H, W, PH * PW, st)
-                          : PxPlan{};
-    const DensePlan dp = (!pp.cg && !xp.cg && path != kPathGeneric) ? dense_plan(C, N, H, W, PH * PW) : DensePlan{};
     int n = 0;
-    if (pp.cg)
-        n = snprintf(name, len, "roi_pool_fwd_pair_kernel<1024, %d, %d, %s>", pp.cg, fx, hb);
-    else if (xp.cg)
-        n = snprintf(name, len, "roi_pool_fwd_wave_kernel<1024, %d, %d, %s>", xp.cg, fx, hb);
-    else if (dp.cg)
-        n = snprintf(name, len, "roi_pool_fwd_dense_kernel<1024, %d, %d, %s, %s>", dp.cg, fx,
-                     (head && rois_sorted) ? "true" : "false", rois_sorted ? "false" : "true");
-    else
-        n = snprintf(name, len, "roi_pool_fwd_kernel<%s>",
-                     (static_cast<size_t>(C) * PH * PW) % 4 == 0 ? "true" : "false");
+    switch (ch.kind) {
+        case kFwdPair: n = snprintf(name, len, "roi_pool_fwd_pair_kernel<1024, %d, %d, %s>", ch.px.cg, fx, hb); break;
+        case kFwdKey: n = snprintf(name, len, "roi_pool_fwd_key_kernel<1024, %d, %d, %s>", ch.px.cg, fx, hb); break;
+        case kFwdWave: n = snprintf(name, len, "roi_pool_fwd_wave_kernel<1024, %d, %d, %s>", ch.px.cg, fx, hb); break;
+        case kFwdDense:
+            n = snprintf(name, len, "roi_pool_fwd_dense_kernel<1024, %d, %d, %s, false>", ch.dn.cg, fx, hb);
+            break;
+        case kFwdDenseList:
+            n = snprintf(name, len, "roi_pool_fwd_dense_kernel<1024, %d, %d, false, true>", ch.dn.cg, fx);
+            break;
+        default:
+            n = snprintf(name, len, "roi_pool_fwd_kernel<%s>",
+                         (static_cast<size_t>(C) * PH * PW) % 4 == 0 ? "true" : "false");
+    }
     return n < 0 ? FRCNN_EINVAL : FRCNN_OK;
 }
 
@@ -2046,40 +2416,20 @@ extern "C" int frcnn_roi_pool_fwd_head(const float* x, const float* rois, const 
     FRCNN_REQUIRE(R <= 0x7fffffff && N <= 65534, "frcnn_roi_pool_fwd_head: too many rois / images");
     if (R == 0) return FRCNN_OK;
     FRCNN_REQUIRE(rois && roi_inds && boxes, "frcnn_roi_pool_fwd_head: null pointer");
-    const int path = path_cfg().roi_fwd;
     const bool aligned = reinterpret_cast<uintptr_t>(rois) % 16 == 0;
-    const PxPlan pp = (rois_sorted && C > 0 && aligned && path == kPathPair)
-                          ? pair_plan(C, N, H, W, PH * PW, as_stream(stream))
-                          : PxPlan{};
-    if (pp.cg) {  // transform + pack inside the pool kernel
-        FRCNN_REQUIRE(x && out && argmax, "frcnn_roi_pool_fwd_head: null pointer");
-        const HeadArgs hd{roi_inds, img_h, img_w, static_cast<float>(H), static_cast<float>(W), boxes};
-        return pair_launch<true>(pp, x, rois, R, N, C, H, W, PH, PW, spatial_scale, out, argmax, hd,
-                                 as_stream(stream));
-    }
-    const PxPlan xp = (rois_sorted && C > 0 && aligned && (path == kPathAuto || path == kPathWave || path == kPathPair))
-                          ? px_plan(C, N, H, W, PH * PW, as_stream(stream))
-                          : PxPlan{};
-    if (xp.cg) {  // transform + pack inside the pool kernel
-        FRCNN_REQUIRE(x && out && argmax, "frcnn_roi_pool_fwd_head: null pointer");
-        const HeadArgs hd{roi_inds, img_h, img_w, static_cast<float>(H), static_cast<float>(W), boxes};
-        return px_launch<true>(xp, x, rois, R, N, C, H, W, PH, PW, spatial_scale, out, argmax, hd,
-                               as_stream(stream));
-    }
-    const DensePlan pl = (rois_sorted && C > 0 && path != kPathGeneric)
-                             ? dense_plan(C, N, H, W, PH * PW)
-                             : DensePlan{};
-    if (!pl.cg || reinterpret_cast<uintptr_t>(rois) % 16 != 0) {
+    const FwdChoice ch = choose_fwd(N, C, H, W, PH, PW, rois_sorted != 0, as_stream(stream));
+    if (!aligned || ch.kind == kFwdDenseList || ch.kind == kFwdGeneric) {
         int rc = frcnn_roi_transform(rois, roi_inds, R, img_h, img_w, H, W, boxes, stream);
         if (rc != FRCNN_OK) return rc;
         if (C == 0) return FRCNN_OK;
         return frcnn_roi_pool_fwd(x, boxes, R, N, C, H, W, PH, PW, spatial_scale, rois_sorted, out,
                                   argmax, workspace, ws_bytes, stream);
     }
+    // transform + pack inside the pool kernel
     FRCNN_REQUIRE(x && out && argmax, "frcnn_roi_pool_fwd_head: null pointer");
     const HeadArgs hd{roi_inds, img_h, img_w, static_cast<float>(H), static_cast<float>(W), boxes};
-    return dense_launch<true, false>(pl, x, rois, nullptr, nullptr, R, N, C, H, W, PH, PW, spatial_scale,
-                                     out, argmax, hd, as_stream(stream));
+    return fwd_tile_launch<true>(ch, x, rois, R, N, C, H, W, PH, PW, spatial_scale, out, argmax, hd,
+                                 as_stream(stream));
 }
 
 namespace {
@@ -2111,6 +2461,59 @@ extern "C" size_t frcnn_roi_pool_bwd_workspace_size(int64_t R, int N, int PH, in
     return carve_bwd(nullptr, R, N, PH, PW).bytes;
 }
 
+namespace {
+// Launch plan of the backward (shared by frcnn_roi_pool_bwd and the name query).
+// Every wave owns one (image, channel) plane and walks all of the image's RoIs,
+// so the work per wave is fixed: spread the N*C waves evenly, one workgroup per
+// CU (ceil(N*C / CUs) waves each) where the LDS allows -- a 2:1 mix of busy and
+// half-idle CUs cost 1.35x.
+struct BwdPlan {
+    bool ring = false, lead = false;
+    int icpw = 1, HWs = 0;
+    size_t lead_bytes = 0;
+};
+BwdPlan bwd_plan(int64_t R, int N, int C, int H, int W, int PH, int PW) {
+    BwdPlan pl;
+    const size_t HW = static_cast<size_t>(H) * W;
+    const size_t plane_bytes = HW * sizeof(float);
+    const int PHW = PH * PW;
+    const int bp = path_cfg().roi_bwd;
+    pl.ring = PHW <= 64 && bp != kPathPlain && plane_bytes <= kPlaneBudgetRing && plane_bytes > 0;
+    if (pl.ring) {
+        const int64_t waves = static_cast<int64_t>(N) * C;
+        int64_t cpw = (waves + device_cu_count() - 1) / device_cu_count();
+        const int64_t lds_cap = static_cast<int64_t>(kPlaneBudgetRing / plane_bytes);
+        cpw = cpw > 16 ? 16 : cpw;
+        cpw = cpw > lds_cap ? lds_cap : cpw;
+        cpw = cpw > C ? C : cpw;
+        cpw = cpw < 1 ? 1 : cpw;
+        pl.icpw = static_cast<int>(cpw);
+        const bool fits = static_cast<uint64_t>(R) * C * PHW * 4 < (1ull << 31);
+        pl.HWs = static_cast<int>((HW + 64 + 3) & ~static_cast<size_t>(3));  // + dummy words
+        pl.lead_bytes = static_cast<size_t>(pl.icpw) * (pl.HWs * sizeof(float) + 2 * kBwdXRow * 8);
+        pl.lead = fits && bp == kPathAuto && PHW < 64 && PW == 7 && pl.lead_bytes <= kPlaneBudgetRing;
+    }
+    return pl;
+}
+}  // namespace
+
+extern "C" int frcnn_roi_pool_bwd_kernel(int64_t R, int N, int C, int H, int W, int PH, int PW, char* name,
+                                         size_t len) {
+    FRCNN_REQUIRE(name && len > 0, "frcnn_roi_pool_bwd_kernel: null name");
+    FRCNN_REQUIRE(R >= 0 && N >= 0 && C >= 0 && H >= 0 && W >= 0 && PH > 0 && PW > 0,
+                  "frcnn_roi_pool_bwd_kernel: bad shape");
+    const BwdPlan pl = bwd_plan(R, N, C, H, W, PH, PW);
+    const size_t plane_bytes = static_cast<size_t>(H) * W * sizeof(float);
+    int n;
+    if (pl.lead)
+        n = snprintf(name, len, "roi_pool_bwd_lead_kernel<%d, 7>", kBwdLead);
+    else if (pl.ring)
+        n = snprintf(name, len, "roi_pool_bwd_pf_kernel<%d>", kBwdRing);
+    else
+        n = snprintf(name, len, "roi_pool_bwd_kernel<%s>", plane_bytes <= kPlaneBudget ? "true" : "false");
+    return n < 0 ? FRCNN_EINVAL : FRCNN_OK;
+}
+
 extern "C" int frcnn_roi_pool_bwd(const float* grad, const float* rois, const int32_t* argmax,
                                   int64_t R, int N, int C, int H, int W, int PH, int PW,
                                   float spatial_scale, float* grad_in, void* workspace,
@@ -2132,32 +2535,12 @@ extern "C" int frcnn_roi_pool_bwd(const float* grad, const float* rois, const in
     FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_bwd: workspace %zu < %zu",
                   ws_bytes, w.bytes);
     FRCNN_REQUIRE(N <= 65535, "frcnn_roi_pool_bwd: N > 65535");
-    const size_t plane_bytes = HW * sizeof(float);
+    const BwdPlan pl = bwd_plan(R, N, C, H, W, PH, PW);
     const int PHW = PH * PW;
-    const int bp = path_cfg().roi_bwd;
-    const bool ring = PHW <= 64 && bp != kPathPlain && plane_bytes <= kPlaneBudgetRing;
-    // Every wave owns one (image, channel) plane and walks all of the image's
-    // RoIs, so the work per wave is fixed: spread the N*C waves evenly, one
-    // workgroup per CU (ceil(N*C / CUs) waves each) where the LDS allows -- a
-    // 2:1 mix of busy and half-idle CUs cost 1.35x.
-    int icpw = 1;
-    bool lead = false;
-    int HWs = 0;
-    size_t lead_bytes = 0;
-    if (ring) {
-        const int64_t waves = static_cast<int64_t>(N) * C;
-        int64_t cpw = (waves + device_cu_count() - 1) / device_cu_count();
-        const int64_t lds_cap = static_cast<int64_t>(kPlaneBudgetRing / plane_bytes);
-        cpw = cpw > 16 ? 16 : cpw;
-        cpw = cpw > lds_cap ? lds_cap : cpw;
-        cpw = cpw > C ? C : cpw;
-        cpw = cpw < 1 ? 1 : cpw;
-        icpw = static_cast<int>(cpw);
-        const bool fits = static_cast<uint64_t>(R) * C * PHW * 4 < (1ull << 31);
-        HWs = static_cast<int>((HW + 64 + 3) & ~static_cast<size_t>(3));  // + dummy words
-        lead_bytes = static_cast<size_t>(icpw) * (HWs * sizeof(float) + 2 * kBwdXRow * 8);
-        lead = fits && bp == kPathAuto && PHW < 64 && PW == 7 && lead_bytes <= kPlaneBudgetRing;
-    }
+    const size_t plane_bytes = HW * sizeof(float);
+    const bool ring = pl.ring, lead = pl.lead;
+    const int icpw = pl.icpw, HWs = pl.HWs;
+    const size_t lead_bytes = pl.lead_bytes;
     if (lead) {  // lists (entries flagged from the geometry) and masks / codes in one launch
         const unsigned grid = static_cast<unsigned>(N + 1 + (R + 15) / 16);
         hipLaunchKernelGGL(roi_bwd_prep_lists_kernel, dim3(grid), dim3(1024), 0, st, rois, static_cast<int>(R), N, H,

@@ -1044,13 +1044,13 @@ extern "C" int frcnn_anchor_target_prepare(int N, int A, int G, const float* anc
 extern "C" int frcnn_anchor_target_draw(int N, int A, int G, int n_sample, double pos_ratio, uint32_t* rng_state,
                                         void* workspace, size_t ws_bytes, void* stream) {
     FRCNN_REQUIRE(N > 0 && N <= 65535 && A > 0 && G >= 0 && G <= kMaxG,
-                  "frcnn_anchor_target_sample: need 0 < N <= 65535, A > 0, 0 <= G <= %d", kMaxG);
+                  "frcnn_anchor_target_draw: need 0 < N <= 65535, A > 0, 0 <= G <= %d", kMaxG);
     const int n_pos_max = static_cast<int>(pos_ratio * n_sample);  // int(0.5*256) (utils/utils.py:190)
-    FRCNN_REQUIRE(n_sample - (n_pos_max < 0 ? 0 : n_pos_max) <= kMaxKeep && n_pos_max <= kMaxKeep,
-                  "frcnn_anchor_target_sample: n_sample too large");
+    FRCNN_REQUIRE(n_sample > 0 && n_sample - (n_pos_max < 0 ? 0 : n_pos_max) <= kMaxKeep && n_pos_max <= kMaxKeep,
+                  "frcnn_anchor_target_draw: n_sample must be in 1..%d per choice() call", kMaxKeep);
     const int Gp = G > 0 ? G : 1;
     AtWs w = carve_at(workspace, N, A, Gp);
-    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_anchor_target_sample: workspace %zu < %zu",
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_anchor_target_draw: workspace %zu < %zu",
                   ws_bytes, w.bytes);
     hipStream_t st = as_stream(stream);
     if (rng_state) {
@@ -1059,7 +1059,7 @@ extern "C" int frcnn_anchor_target_draw(int N, int A, int G, int n_sample, doubl
         FRCNN_LAUNCH_CHECK("at_sample_kernel");
     } else if (hipMemsetAsync(w.sampled, 0, sizeof(int) * 2 * N, st) != hipSuccess ||
                hipMemsetAsync(w.calls, 0, sizeof(int4) * 2 * N, st) != hipSuccess) {
-        return check_launch("frcnn_anchor_target_sample memset");
+        return check_launch("frcnn_anchor_target_draw memset");
     }
     return FRCNN_OK;
 }
@@ -1068,11 +1068,11 @@ extern "C" int frcnn_anchor_target_finish(int N, int A, int G, const float* anch
                                           int32_t* argmax, double* max_iou, void* workspace, size_t ws_bytes,
                                           void* stream) {
     FRCNN_REQUIRE(N > 0 && N <= 65535 && A > 0 && G >= 0 && G <= kMaxG,
-                  "frcnn_anchor_target_sample: need 0 < N <= 65535, A > 0, 0 <= G <= %d", kMaxG);
-    FRCNN_REQUIRE(anchors && reg && label, "frcnn_anchor_target_sample: null pointer");
+                  "frcnn_anchor_target_finish: need 0 < N <= 65535, A > 0, 0 <= G <= %d", kMaxG);
+    FRCNN_REQUIRE(anchors && reg && label, "frcnn_anchor_target_finish: null pointer");
     const int Gp = G > 0 ? G : 1;
     AtWs w = carve_at(workspace, N, A, Gp);
-    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_anchor_target_sample: workspace %zu < %zu",
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_anchor_target_finish: workspace %zu < %zu",
                   ws_bytes, w.bytes);
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(samp_emit_kernel<0>, dim3(2 * N), dim3(kSampThreads), 0, st, w.calls, w.jrec, w.pos_list,
@@ -1084,10 +1084,10 @@ extern "C" int frcnn_anchor_target_finish(int N, int A, int G, const float* anch
     FRCNN_LAUNCH_CHECK("at_finish_kernel");
     if (argmax && hipMemcpyAsync(argmax, w.row_arg, sizeof(int32_t) * N * A,
                                  hipMemcpyDeviceToDevice, st) != hipSuccess)
-        return check_launch("frcnn_anchor_target_sample copy");
+        return check_launch("frcnn_anchor_target_finish copy");
     if (max_iou && hipMemcpyAsync(max_iou, w.row_max, sizeof(double) * N * A,
                                   hipMemcpyDeviceToDevice, st) != hipSuccess)
-        return check_launch("frcnn_anchor_target_sample copy");
+        return check_launch("frcnn_anchor_target_finish copy");
     return FRCNN_OK;
 }
 
@@ -1167,14 +1167,14 @@ extern "C" int frcnn_proposal_target_prepare(int N, int Rp, const float* rois, c
                                              double neg_iou_thresh_low, void* workspace, size_t ws_bytes,
                                              void* stream) {
     FRCNN_REQUIRE(N > 0 && N <= 65535 && Rp >= 0 && G >= 0 && G <= kMaxG && n_sample > 0,
-                  "frcnn_proposal_target: bad shape");
-    FRCNN_REQUIRE(Rp + G <= kMaxKeep, "frcnn_proposal_target: rois + gt must be <= %d", kMaxKeep);
-    FRCNN_REQUIRE(rcount, "frcnn_proposal_target: null pointer");
-    FRCNN_REQUIRE(Rp == 0 || rois, "frcnn_proposal_target: null rois");
-    FRCNN_REQUIRE(G == 0 || (boxes && labels), "frcnn_proposal_target: null boxes");
+                  "frcnn_proposal_target_prepare: bad shape");
+    FRCNN_REQUIRE(Rp + G <= kMaxKeep, "frcnn_proposal_target_prepare: rois + gt must be <= %d", kMaxKeep);
+    FRCNN_REQUIRE(rcount, "frcnn_proposal_target_prepare: null pointer");
+    FRCNN_REQUIRE(Rp == 0 || rois, "frcnn_proposal_target_prepare: null rois");
+    FRCNN_REQUIRE(G == 0 || (boxes && labels), "frcnn_proposal_target_prepare: null boxes");
     const int Gp = G > 0 ? G : 1;
     PtWs w = carve_pt(workspace, N, Rp, Gp, n_sample);
-    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_proposal_target: workspace %zu < %zu",
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_proposal_target_prepare: workspace %zu < %zu",
                   ws_bytes, w.bytes);
     hipStream_t st = as_stream(stream);
     if (G > 0) {
@@ -1194,11 +1194,13 @@ extern "C" int frcnn_proposal_target_prepare(int N, int Rp, const float* rois, c
 extern "C" int frcnn_proposal_target_draw(int N, int Rp, int G, int n_sample, double pos_ratio, uint32_t* rng_state,
                                           int32_t* sample_count, void* workspace, size_t ws_bytes, void* stream) {
     FRCNN_REQUIRE(N > 0 && N <= 65535 && Rp >= 0 && G >= 0 && G <= kMaxG && n_sample > 0,
-                  "frcnn_proposal_target: bad shape");
-    FRCNN_REQUIRE(rng_state && sample_count, "frcnn_proposal_target: null pointer");
+                  "frcnn_proposal_target_draw: bad shape");
+    // the recorded swaps of one choice() call fill one [kMaxKeep] row of jrec
+    FRCNN_REQUIRE(Rp + G <= kMaxKeep, "frcnn_proposal_target_draw: rois + gt must be <= %d", kMaxKeep);
+    FRCNN_REQUIRE(rng_state && sample_count, "frcnn_proposal_target_draw: null pointer");
     const int Gp = G > 0 ? G : 1;
     PtWs w = carve_pt(workspace, N, Rp, Gp, n_sample);
-    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_proposal_target: workspace %zu < %zu",
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_proposal_target_draw: workspace %zu < %zu",
                   ws_bytes, w.bytes);
     hipStream_t st = as_stream(stream);
     const int stride = Rp + Gp;
@@ -1215,12 +1217,13 @@ extern "C" int frcnn_proposal_target_finish(int N, int Rp, int G, int n_sample, 
                                             double* sample_roi, double* gt_roi_reg, double* gt_roi_label,
                                             void* workspace, size_t ws_bytes, void* stream) {
     FRCNN_REQUIRE(N > 0 && N <= 65535 && Rp >= 0 && G >= 0 && G <= kMaxG && n_sample > 0,
-                  "frcnn_proposal_target: bad shape");
+                  "frcnn_proposal_target_finish: bad shape");
+    FRCNN_REQUIRE(Rp + G <= kMaxKeep, "frcnn_proposal_target_finish: rois + gt must be <= %d", kMaxKeep);
     FRCNN_REQUIRE(sample_roi && gt_roi_reg && gt_roi_label && sample_count && reg_mean && reg_std,
-                  "frcnn_proposal_target: null pointer");
+                  "frcnn_proposal_target_finish: null pointer");
     const int Gp = G > 0 ? G : 1;
     PtWs w = carve_pt(workspace, N, Rp, Gp, n_sample);
-    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_proposal_target: workspace %zu < %zu",
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_proposal_target_finish: workspace %zu < %zu",
                   ws_bytes, w.bytes);
     hipStream_t st = as_stream(stream);
     const int stride = Rp + Gp;
@@ -1245,7 +1248,7 @@ extern "C" int frcnn_proposal_target_sample(int N, int Rp, int G, int n_sample, 
                                             double* gt_roi_label, int32_t* sample_count, void* workspace,
                                             size_t ws_bytes, void* stream) {
     FRCNN_REQUIRE(sample_roi && gt_roi_reg && gt_roi_label && reg_mean && reg_std,
-                  "frcnn_proposal_target: null pointer");
+                  "frcnn_proposal_target_sample: null pointer");
     const int rc = frcnn_proposal_target_draw(N, Rp, G, n_sample, pos_ratio, rng_state, sample_count, workspace,
                                               ws_bytes, stream);
     if (rc != FRCNN_OK) return rc;
