@@ -731,6 +731,9 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
                                 mv[4 * q + j] = vv[j];
                                 mi[4 * q + j] = ii;
                             }
+#ifdef FRCNN_WAVE_VCC
+                            __builtin_amdgcn_sched_barrier(0);
+#endif
                         }
                     }
                 }
@@ -1001,8 +1004,12 @@ __device__ unsigned long long g_key_prof[4];  // fast RoI-waves, re-scanning wav
 #define KPROF(i, v) do {} while (0)
 #endif
 #ifndef FRCNN_KEY_DBG
-#define FRCNN_KEY_DBG 0  // experiment builds only: 1 no check, 2 no K pass, 4 no stores
+#define FRCNN_KEY_DBG 0  // experiment builds only: 1 no check, 2 no K pass, 4 no stores, 8 fake check
 #endif
+#ifndef FRCNN_KEY_NT
+#define FRCNN_KEY_NT 1024
+#endif
+constexpr int kKeyNT = FRCNN_KEY_NT;  // threads per key-kernel workgroup
 constexpr int kKeyBits = 10;
 constexpr uint32_t kKeyMask = (1u << kKeyBits) - 1;
 constexpr uint32_t kKeyZero = 0x80000001u;  // pool_key(+0.0f): the empty-window sentinel
@@ -1010,6 +1017,14 @@ constexpr uint32_t kKeyZero = 0x80000001u;  // pool_key(+0.0f): the empty-window
 __device__ __forceinline__ uint32_t pool_key(float v) {
     const uint32_t u = __float_as_uint(v);
     return (u ^ (static_cast<uint32_t>(static_cast<int32_t>(u) >> 31) | 0x80000000u)) + 1u;
+}
+// (key & ~kKeyMask) | code as one v_bitop3_b32 (truth table 0xDC on
+// (key, code, mask)): measured 2.7 cycles per wave64 instruction at 4 waves per
+// SIMD against 4.7 for v_and_or_b32 (tools/valu_rate2.hip).
+__device__ __forceinline__ uint32_t key_code(uint32_t key, uint32_t code, uint32_t low_mask) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xdc" : "=v"(r) : "v"(key), "v"(code), "s"(low_mask));
+    return r;
 }
 __device__ __forceinline__ uint32_t pool_unkey(uint32_t k) {
     const uint32_t u = k - 1u;
@@ -1169,6 +1184,29 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_key_kernel(
         if (tid == 0) s_next = 0;
         __syncthreads();
         if (k0 == 0) PPROF_T(2);
+        // paced output: RoI t-1's 2*CG stores go out 4 at a time between RoI t's
+        // scan steps (kPace), so the store queue is fed evenly instead of in
+        // 32-store bursts the waves would all wait behind
+        constexpr bool kPace = (FRCNN_KEY_DBG & 32) != 0;
+        constexpr int kBlk = CG / 2;
+        float pv[CG];
+        uint32_t pi2[CG / 2];  // argmax pairs, 16 bits each (|argmax| < H * W + 1 <= 32768)
+        size_t po = 0;
+        int pblk = kBlk;  // blocks of the pending RoI not yet stored (kBlk: none pending)
+        auto pace = [&](int bb_) {
+            if (act) {
+                float* op = out + po;
+                int32_t* ap = argmax + po;
+#pragma unroll
+                for (int bb = 0; bb < kBlk; ++bb)
+                    if (bb == bb_) {
+                        op[(2 * bb) * PHW] = pv[2 * bb];
+                        ap[(2 * bb) * PHW] = static_cast<int>(static_cast<int16_t>(pi2[bb] & 0xFFFFu));
+                        op[(2 * bb + 1) * PHW] = pv[2 * bb + 1];
+                        ap[(2 * bb + 1) * PHW] = static_cast<int>(pi2[bb]) >> 16;
+                    }
+            }
+        };
         int k = 0;
         if (lane == 0) k = atomicAdd(&s_next, 1);
         k = __builtin_amdgcn_readfirstlane(k);
@@ -1197,6 +1235,7 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_key_kernel(
                 KPROF(0, 1);
                 const int hh1 = empty ? 0 : g.y - g.x - 1, ww1 = empty ? 0 : g.w - g.z - 1;
                 const uint32_t cb = static_cast<uint32_t>(p0) + kKeyMask;
+                const uint32_t kmask = __builtin_amdgcn_readfirstlane(kKeyMask);  // SGPR operand of key_code
                 uint32_t K[CG], M[CG];
 #pragma unroll
                 for (int c = 0; c < CG; ++c) K[c] = M[c] = 0u;
@@ -1221,11 +1260,12 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_key_kernel(
                             const uint32_t tb[4] = {vb[q].x, vb[q].y, vb[q].z, vb[q].w};
 #pragma unroll
                             for (int j = 0; j < 4; ++j) {
-                                const uint32_t ka = (ta[j] & ~kKeyMask) | ca, kb = (tb[j] & ~kKeyMask) | cc;
+                                const uint32_t ka = key_code(ta[j], ca, kmask), kb = key_code(tb[j], cc, kmask);
                                 if (!(FRCNN_KEY_DBG & 2)) K[4 * q + j] = max(K[4 * q + j], max(ka, kb));
                                 M[4 * q + j] = max(M[4 * q + j], max(ta[j], tb[j]));
                             }
                         }
+                        if (kPace && pblk < kBlk) pace(pblk++);
                     }
                     if (dw < wmax) {  // odd width: the last column alone
                         const int pa = rb + min(dw, ww1);
@@ -1240,46 +1280,68 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_key_kernel(
                             const uint32_t ta[4] = {va[q].x, va[q].y, va[q].z, va[q].w};
 #pragma unroll
                             for (int j = 0; j < 4; ++j) {
-                                if (!(FRCNN_KEY_DBG & 2)) K[4 * q + j] = max(K[4 * q + j], (ta[j] & ~kKeyMask) | ca);
+                                if (!(FRCNN_KEY_DBG & 2)) K[4 * q + j] = max(K[4 * q + j], key_code(ta[j], ca, kmask));
                                 M[4 * q + j] = max(M[4 * q + j], ta[j]);
                             }
                         }
+                        if (kPace && pblk < kBlk) pace(pblk++);
                     }
                 }
                 // the first pixel of the maximum's class and the check of its key
                 // against the maximum (LDS: a reload from memory would wait, in
                 // vmcnt order, for the previous RoI's stores); an empty window
                 // names the sentinel pixel (key +0.0 = its maximum) and argmax -1
+                // (ds_read_b128 of the named pixel's 4-channel quad: its 16-B slots
+                // spread over all 64 banks; a dword read of one channel would hit
+                // 8 of 32 banks)
                 const int ioff = empty ? -(HW + 1) : 0;
                 uint32_t bad = 0;
 #pragma unroll
                 for (int c = 0; c < CG; ++c) {
                     const int p = static_cast<int>(cb - (K[c] & kKeyMask));
                     idx[c] = p + ioff;
-                    if (!(FRCNN_KEY_DBG & 1)) {
-                        const uint32_t t = reinterpret_cast<const uint32_t*>(tile_px<NP>(t4, p))[64 * (c / 4) + (c % 4)];
+                    if (FRCNN_KEY_DBG & 8) bad |= K[c] == 0xFFFFFFFFu;  // experiment: keep the re-scan, no reads
+                    if (!(FRCNN_KEY_DBG & 9)) {
+                        const uint4 t4q = reinterpret_cast<const uint4*>(tile_px<NP>(t4, p))[16 * (c / 4)];
+                        const uint32_t t = (c % 4) == 0 ? t4q.x : (c % 4) == 1 ? t4q.y : (c % 4) == 2 ? t4q.z : t4q.w;
                         bad |= t ^ M[c];
                     }
                     val[c] = __uint_as_float(pool_unkey(M[c]));
                 }
                 if (__builtin_amdgcn_ballot_w64(bad != 0)) {
                     KPROF(1, 1);
-                    KPROF(2, __builtin_popcountll(__builtin_amdgcn_ballot_w64(bad != 0)));
+                    { const auto bl = __builtin_amdgcn_ballot_w64(bad != 0); KPROF(2, __builtin_popcountll(bl)); }
                     if (bad) key_exact<NP>(k4, p0, empty ? 0 : g.y - g.x, empty ? 0 : g.w - g.z, W, val, idx);
                 }
             }
-            if (act && !(FRCNN_KEY_DBG & 4)) {
+            if (kPace) {
+                while (pblk < kBlk) pace(pblk++);
+#pragma unroll
+                for (int c = 0; c < CG; ++c) pv[c] = val[c];
+#pragma unroll
+                for (int c = 0; c < CG / 2; ++c)
+                    pi2[c] = (static_cast<uint32_t>(idx[2 * c]) & 0xFFFFu) | (static_cast<uint32_t>(idx[2 * c + 1]) << 16);
+                po = (static_cast<size_t>(r) * C + c0) * PHW + lane;
+                pblk = 0;
+            } else if (act && !(FRCNN_KEY_DBG & 4)) {
                 const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
                 float* op = out + o;
                 int32_t* ap = argmax + o;
 #pragma unroll
                 for (int c = 0; c < CG; ++c) {
-                    op[c * PHW] = val[c];
-                    ap[c * PHW] = idx[c];
+                    if (FRCNN_KEY_DBG & 16) {
+                        __builtin_nontemporal_store(val[c], op + c * PHW);
+                        __builtin_nontemporal_store(idx[c], ap + c * PHW);
+                    } else {
+                        op[c * PHW] = val[c];
+                        ap[c * PHW] = idx[c];
+                    }
                 }
             }
             k = __builtin_amdgcn_readfirstlane(kn);
         }
+        if (kPace)
+            while (pblk < kBlk) pace(pblk++);
         __syncthreads();  // the chunk's geometry and s_next are reused
     }
     PPROF_T(3);
@@ -2146,7 +2208,7 @@ int key_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, i
     const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(pl.split), static_cast<unsigned>(N + 1));
     const bool fix7 = PH == 7 && PW == 7;
 #define FRCNN_KEY(CG, FX)                                                                                  \
-    hipLaunchKernelGGL((roi_pool_fwd_key_kernel<1024, CG, FX, HEAD>), grid, dim3(1024), pl.lds, st, x, rois, \
+    hipLaunchKernelGGL((roi_pool_fwd_key_kernel<kKeyNT, CG, FX, HEAD>), grid, dim3(kKeyNT), pl.lds, st, x, rois, \
                        static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd)
     if (pl.cg == 16) {
         if (fix7) FRCNN_KEY(16, 7); else FRCNN_KEY(16, 0);
@@ -2390,7 +2452,7 @@ extern "C" int frcnn_roi_pool_fwd_kernel(int64_t R, int N, int C, int H, int W, 
     int n = 0;
     switch (ch.kind) {
         case kFwdPair: n = snprintf(name, len, "roi_pool_fwd_pair_kernel<1024, %d, %d, %s>", ch.px.cg, fx, hb); break;
-        case kFwdKey: n = snprintf(name, len, "roi_pool_fwd_key_kernel<1024, %d, %d, %s>", ch.px.cg, fx, hb); break;
+        case kFwdKey: n = snprintf(name, len, "roi_pool_fwd_key_kernel<%d, %d, %d, %s>", kKeyNT, ch.px.cg, fx, hb); break;
         case kFwdWave: n = snprintf(name, len, "roi_pool_fwd_wave_kernel<1024, %d, %d, %s>", ch.px.cg, fx, hb); break;
         case kFwdDense:
             n = snprintf(name, len, "roi_pool_fwd_dense_kernel<1024, %d, %d, %s, false>", ch.dn.cg, fx, hb);

@@ -22,6 +22,7 @@ rois, idx, cnt = ops.propose(sc, de, img_w=c["img_w"], img_h=c["img_h"], pre_nms
                              post_nms=c["post_nms"], anchor_base=base, feat_h=c["feat_h"], feat_w=c["feat_w"])
 inds = torch.arange(N, device=dev, dtype=torch.float32).repeat_interleave(c["post_nms"])
 lib = _lib.load()
+_lib.set_path("roi_pool_fwd", "key")
 buf = (ctypes.c_ulonglong * 4)()
 lib.frcnn_debug_key_prof(buf, 1)
 ops.roi_pool_head(x, rois.view(-1, 4), inds, 7, c["img_h"], c["img_w"], rois_sorted=True)
