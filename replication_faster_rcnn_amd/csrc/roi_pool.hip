@@ -731,9 +731,6 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
                                 mv[4 * q + j] = vv[j];
                                 mi[4 * q + j] = ii;
                             }
-#ifdef FRCNN_WAVE_VCC
-                            __builtin_amdgcn_sched_barrier(0);
-#endif
                         }
                     }
                 }
