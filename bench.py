@@ -77,11 +77,15 @@ def parse():
     ap.add_argument("--prop-streams", type=int, default=4,
                     help="with --streams 2 (inference configs): proposal layers of consecutive "
                          "steps round-robin over this many HIP streams")
-    ap.add_argument("--pool-on", default="prop", choices=("prop", "own"),
+    ap.add_argument("--prop-prio", type=int, default=0,
+                    help="HIP stream priority of the proposal streams (negative = higher; with "
+                         "--pool-on split the RoIPool streams keep the default)")
+    ap.add_argument("--pool-on", default="prop", choices=("prop", "own", "split"),
                     help="with --streams 2 (inference): prop = each step's RoIPool runs on that step's "
                          "proposal stream right after its proposals (consecutive steps on different "
                          "streams overlap; no cross-stream waits), own = the RoIPool on a stream of "
-                         "its own, fed by events")
+                         "its own, fed by events, split = each proposal stream's RoIPool on a "
+                         "companion stream of its own (events)")
     ap.add_argument("--prop-cus", type=int, default=0,
                     help="with --streams 2: CUs reserved for the proposal streams (spread over the "
                          "XCDs); the RoIPool stream gets the rest.  0 = no reservation")
@@ -364,6 +368,9 @@ def make_streams(args):
         s = torch.cuda.current_stream()
         return [s], s
     nps = max(1, args.prop_streams)
+    if args.pool_on == "split":  # a RoIPool stream per proposal stream
+        props = [torch.cuda.Stream(priority=args.prop_prio) for _ in range(nps)]
+        return props, [torch.cuda.Stream() for _ in range(nps)]
     if args.prop_cus > 0:
         from replication_faster_rcnn_amd import _lib
         n = _lib.cu_count()
@@ -371,7 +378,7 @@ def make_streams(args):
         rest = [i for i in range(n) if i not in set(res)]
         pool = _lib.cu_stream(rest) if args.mask_pool else torch.cuda.Stream()
         return [_lib.cu_stream(res) for _ in range(nps)], pool
-    return [torch.cuda.Stream() for _ in range(nps)], torch.cuda.Stream()
+    return [torch.cuda.Stream(priority=args.prop_prio) for _ in range(nps)], torch.cuda.Stream()
 
 
 def inference_step_fn(args, c, sets, base, world, n_total, backend, ev):
@@ -390,7 +397,9 @@ def inference_step_fn(args, c, sets, base, world, n_total, backend, ev):
     nps = len(s_props)
     home = torch.cuda.current_stream()
     on_prop = [_On(sp, home) for sp in s_props]
-    on_pool = _On(s_pool, home)
+    split = isinstance(s_pool, list)  # --pool-on split: one RoIPool stream per proposal stream
+    s_pools = s_pool if split else [s_pool] * nps
+    on_pools = [_On(sp, home) for sp in s_pools]
     gathers = None
     if world > 1:  # proposals written straight into each stream's preallocated send buffer
         from replication_faster_rcnn_amd import dist as fdist
@@ -409,7 +418,7 @@ def inference_step_fn(args, c, sets, base, world, n_total, backend, ev):
     pool_outs = [(torch.empty((N * post, C, 7, 7), dtype=torch.float32, device=dev),
                   torch.empty((N * post, C, 7, 7), dtype=torch.int32, device=dev),
                   torch.empty((N * post, 5), dtype=torch.float32, device=dev))
-                 for _ in range(nps if pool_on_prop else 1)]
+                 for _ in range(nps if (pool_on_prop or split) else 1)]
     pool_out = pool_outs[0]
     ready = [torch.cuda.Event() for _ in range(nps)]
     done = [None] * nps          # the pool that last read prop_out[j]
@@ -476,7 +485,8 @@ def inference_step_fn(args, c, sets, base, world, n_total, backend, ev):
             if args.host_io:
                 h_rois.copy_(rois, non_blocking=True)
             ready[j].record(s_prop)
-        with on_pool:
+        s_pool, pool_out = s_pools[j], pool_outs[j if split else 0]
+        with on_pools[j]:
             s_pool.wait_event(ready[j])
             if timed:
                 e0, e1 = ev["pairs"][ev["i"]]
@@ -503,7 +513,7 @@ def inference_step_fn(args, c, sets, base, world, n_total, backend, ev):
     step.alone = alone
     from replication_faster_rcnn_amd import _lib
     step.kernel = _lib.roi_pool_fwd_kernel(N * post, N, C, x.size(2), x.size(3),
-                                           stream=s_props[0] if pool_on_prop else s_pool)
+                                           stream=s_props[0] if pool_on_prop else s_pools[0])
     return step
 
 
