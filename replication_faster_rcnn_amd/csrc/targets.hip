@@ -289,8 +289,14 @@ __device__ unsigned long long g_samp_prof[16];
 #define SPROF_DT(k) do {} while (0)
 #endif
 constexpr int kWinWaves = 12;              // waves that walk a window; the other 4 twist ahead
-constexpr int kWin = kWinWaves * 64;       // words per window
-constexpr int kRing = 4;  // a window (768 words from pos <= 624) spans <= 3 blocks, + 1 being twisted
+#ifndef FRCNN_SAMP_SUBC
+#define FRCNN_SAMP_SUBC 1
+#endif
+constexpr int kSubc = FRCNN_SAMP_SUBC;     // 64-word chunks per walking wave and window
+constexpr int kWinChunks = kWinWaves * kSubc;
+constexpr int kWin = kWinChunks * 64;      // words per window
+// a window (kWin words from pos <= 624) spans <= (624 + kWin - 1) / 624 + 1 blocks, + 1 being twisted
+constexpr int kRing = (kMtN + kWin - 1) / kMtN + 2;
 #ifndef FRCNN_SEQ_BELOW
 #define FRCNN_SEQ_BELOW 1024
 #endif
@@ -374,7 +380,8 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
         // others walk the window; the window's barriers publish it
         const bool gen = st.ngen < kRing - 1;
         if (gen && wid >= kWinWaves)
-            mt_twist(S.ring[(st.slot + st.ngen) % kRing], S.ring[(st.slot + st.ngen + 1) % kRing], tid - kWin);
+            mt_twist(S.ring[(st.slot + st.ngen) % kRing], S.ring[(st.slot + st.ngen + 1) % kRing],
+                     tid - kWinWaves * 64);
         SPROF_ADD(0, 1);
         SPROF_T0();
         if (i_cur < kSeqBelow) {
@@ -389,9 +396,9 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
                     return S.ring[(st.slot + bc) % kRing][gc - bc * kMtN];
                 };
                 uint32_t wn = word(0);  // the next chunk's word is read during this one's fixed point
-                for (int c = 0; c < kWinWaves && i_loc >= 1; ++c) {
+                for (int c = 0; c < kWinChunks && i_loc >= 1; ++c) {
                     const uint32_t wc = mt_temper(wn);
-                    if (c + 1 < kWinWaves) wn = word(c + 1);
+                    if (c + 1 < kWinChunks) wn = word(c + 1);
                     // (a guess: any start reaches the same fixed point, so the
                     // approximate reciprocal, not the IEEE division the build flags make '/')
                     const float pa = (static_cast<float>(i_loc) + 1.0f) *
@@ -438,19 +445,27 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
             __syncthreads();
             continue;
         }
-        const int g = st.off + (wid < kWinWaves ? tid : 0);
-        const int blk = g / kMtN;
-        const uint32_t w = mt_temper(S.ring[(st.slot + blk) % kRing][g - blk * kMtN]);
+        // wave wid walks chunks wid * kSubc .. + kSubc - 1 (64 words each, in
+        // stream order); its fixed point runs over all of them (Gauss-Seidel:
+        // each chunk's steps from the counts of the chunks before it)
+        uint32_t w[kSubc];
+#pragma unroll
+        for (int sc = 0; sc < kSubc; ++sc) {
+            const int g = st.off + (wid < kWinWaves ? (wid * kSubc + sc) * 64 + lane : 0);
+            const int blk = g / kMtN;
+            w[sc] = mt_temper(S.ring[(st.slot + blk) % kRing][g - blk * kMtN]);
+        }
         const float p_acc = (static_cast<float>(i_cur) + 1.0f) *
                             __builtin_amdgcn_rcpf(static_cast<float>(mask_for(static_cast<uint32_t>(i_cur))) + 1.0f);
         auto guess = [&](int v) { return static_cast<int>(static_cast<float>(v * 64) * p_acc); };
-        int base = guess(wid);
-        uint64_t acc;
-        {
-            const int ig = i_cur - base - static_cast<int>(static_cast<float>(lane) * p_acc);
-            acc = __ballot(ig >= 1 && (w & mask_for(static_cast<uint32_t>(ig))) <= static_cast<uint32_t>(ig));
+        int base = guess(wid * kSubc);
+        uint64_t acc[kSubc];
+#pragma unroll
+        for (int sc = 0; sc < kSubc; ++sc) {
+            const int ig = i_cur - base - static_cast<int>(static_cast<float>(sc * 64 + lane) * p_acc);
+            acc[sc] = __ballot(ig >= 1 && (w[sc] & mask_for(static_cast<uint32_t>(ig))) <= static_cast<uint32_t>(ig));
         }
-        // Round: each unsettled wave solves its 64 words for its assumed base and
+        // Round: each unsettled wave solves its words for its assumed base and
         // publishes (count, margins, base): its pattern stays exact for any base in
         // [base - up, base + down] (no word changes its decision or mask width).
         // The first wave whose exact base (prefix of the counts before it) falls
@@ -458,44 +473,69 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
         // the new prefix; the waves before it are settled.  Counts hardly depend on
         // the base, so the first round's guesses are usually inside the margins and
         // the rest settle in the second; each round settles at least one more wave.
-        int il = 0, total = 0, par = 0;
-        uint32_t m = 0;
-        bool a = false, done = wid >= kWinWaves;  // the twisting waves only keep the barriers
+        int il[kSubc], total = 0, par = 0;
+        uint32_t m[kSubc];
+        bool a[kSubc];
+#pragma unroll
+        for (int sc = 0; sc < kSubc; ++sc) {
+            il[sc] = 0;
+            m[sc] = 0;
+            a[sc] = false;
+        }
+        bool done = wid >= kWinWaves;  // the twisting waves only keep the barriers
         for (;;) {  // rounds
             if (!done) {
-                for (;;) {  // this wave's 64 words, exact for the assumed `base`
-                    const int below = static_cast<int>(__builtin_amdgcn_mbcnt_hi(
-                        static_cast<uint32_t>(acc >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(acc), 0u)));
-                    il = i_cur - base - below;
-                    const bool valid = il >= 1;
-                    m = mask_for(static_cast<uint32_t>(valid ? il : 1));
-                    a = valid && (w & m) <= static_cast<uint32_t>(il);
-                    const uint64_t nacc = __ballot(a);
-                    if (nacc == acc) break;
-                    acc = nacc;
+                for (;;) {  // this wave's words, exact for the assumed `base`
+                    bool ch = false;
+                    int pre = 0;
+#pragma unroll
+                    for (int sc = 0; sc < kSubc; ++sc) {
+                        const int below = pre + static_cast<int>(__builtin_amdgcn_mbcnt_hi(
+                            static_cast<uint32_t>(acc[sc] >> 32),
+                            __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(acc[sc]), 0u)));
+                        il[sc] = i_cur - base - below;
+                        const bool valid = il[sc] >= 1;
+                        m[sc] = mask_for(static_cast<uint32_t>(valid ? il[sc] : 1));
+                        a[sc] = valid && (w[sc] & m[sc]) <= static_cast<uint32_t>(il[sc]);
+                        const uint64_t nacc = __ballot(a[sc]);
+                        ch |= nacc != acc[sc];
+                        acc[sc] = nacc;
+                        pre += __popcll(nacc);
+                    }
+                    if (!ch) break;
                 }
             }
-            // Margins from the first round on: a wave's 64-word pattern depends on its
+            // Margins from the first round on: a wave's pattern depends on its
             // base only where (w & mask) lies that close to the step, so at wide
             // masks the guessed bases usually fall inside the margins and the window
             // settles in one round (settled waves keep d == 0 and need none).
             uint32_t dn = 0, up = 0;
+            int cnt = 0;
+#pragma unroll
+            for (int sc = 0; sc < kSubc; ++sc) cnt += __popcll(acc[sc]);
             if (!done) {
-                if (il < 1) {
-                    dn = 0x3fffffffu;
-                    up = static_cast<uint32_t>(-il);
-                } else {
-                    const uint32_t lo = (m >> 1) + 1u;  // 2^k of the mask m = 2^(k+1) - 1
-                    const uint32_t v = w & m;
-                    const uint32_t u = static_cast<uint32_t>(il);
-                    dn = a ? u - (v > lo ? v : lo) : u - lo;
-                    up = a ? m - u : v - 1u - u;
+                dn = up = 0x3fffffffu;
+#pragma unroll
+                for (int sc = 0; sc < kSubc; ++sc) {
+                    uint32_t dns, ups;
+                    if (il[sc] < 1) {
+                        dns = 0x3fffffffu;
+                        ups = static_cast<uint32_t>(-il[sc]);
+                    } else {
+                        const uint32_t lo = (m[sc] >> 1) + 1u;  // 2^k of the mask m = 2^(k+1) - 1
+                        const uint32_t v = w[sc] & m[sc];
+                        const uint32_t u = static_cast<uint32_t>(il[sc]);
+                        dns = a[sc] ? u - (v > lo ? v : lo) : u - lo;
+                        ups = a[sc] ? m[sc] - u : v - 1u - u;
+                    }
+                    dn = dns < dn ? dns : dn;
+                    up = ups < up ? ups : up;
                 }
                 dn = __ockl_wfred_min_u32(dn);
                 up = __ockl_wfred_min_u32(up);
             }
             if (lane == 0 && wid < kWinWaves)
-                S.rec[par][wid] = make_int4(__popcll(acc), static_cast<int>(dn), static_cast<int>(up), base);
+                S.rec[par][wid] = make_int4(cnt, static_cast<int>(dn), static_cast<int>(up), base);
             __syncthreads();
             const int4 r = lane < kWinWaves ? S.rec[par][lane] : make_int4(0, 0, 0, 0);
             const int incl = row16_scan_add(r.x);  // lanes 0..15: prefix over waves
@@ -506,7 +546,8 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
             const int my_excl = __builtin_amdgcn_readlane(excl, wid < kWinWaves ? wid : 0);
             if (wid < first_bad) {
                 if (!done) {  // settled: same pattern at the exact base, steps shifted
-                    il -= my_excl - base;
+#pragma unroll
+                    for (int sc = 0; sc < kSubc; ++sc) il[sc] -= my_excl - base;
                     base = my_excl;
                     done = true;
                 }
@@ -519,10 +560,18 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
             if (first_bad == kWinWaves) break;
         }
         SPROF_DT(4);
-        if (a && il >= rec_lo) J[il - rec_lo] = static_cast<int>(w & m);
+#pragma unroll
+        for (int sc = 0; sc < kSubc; ++sc)
+            if (a[sc] && il[sc] >= rec_lo) J[il[sc] - rec_lo] = static_cast<int>(w[sc] & m[sc]);
         int consumed = kWin;
         if (i_cur - total < 1) {  // the call ends inside this window
-            if (lane == 0 && wid < kWinWaves) S.last[wid] = acc ? 64 * wid + 64 - __clzll(acc) : 0;
+            if (lane == 0 && wid < kWinWaves) {
+                int last = 0;
+#pragma unroll
+                for (int sc = 0; sc < kSubc; ++sc)
+                    if (acc[sc]) last = 64 * (wid * kSubc + sc) + 64 - __clzll(acc[sc]);
+                S.last[wid] = last;
+            }
             __syncthreads();
             consumed = static_cast<int>(__ockl_wfred_max_u32(lane < kWinWaves ? static_cast<uint32_t>(S.last[lane]) : 0u));
         }

@@ -34,7 +34,7 @@ run_step() {
     bench)
       local name=$1; shift
       timeout -k 10 400 python -u bench.py "$@" > "$OUT/bench_$name.json" 2>"$OUT/bench_$name.err" || { tail -5 "$OUT/bench_$name.err"; return 1; }
-      python3 -c "import json; d=json.loads(open('$OUT/bench_$name.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$name', round(d['value'],1), 'img/s', round(d['ms_per_step']*1e3,1), 'us/step frac', round(r['frac'],3), 'alone', round(r['kernel_us_alone'],1), 'us', round(r['frac_alone'],3), r.get('kernel'))" ;;
+      python3 -c "import json; d=json.loads(open('$OUT/bench_$name.json').read().strip().splitlines()[-1]); r=d['roofline']; f=lambda v: None if v is None else round(v,3); print('$name', round(d['value'],1), 'img/s', round(d['ms_per_step']*1e3,1), 'us/step', r.get('kernel'), 'achieved', f(r.get('achieved')), 'frac', f(r.get('frac')), 'alone', f(r.get('kernel_us_alone')), f(r.get('frac_alone')))" ;;
     prof)
       local name=$1; shift
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" -o run -- \
