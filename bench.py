@@ -596,29 +596,29 @@ def train_step_fn(args, c, sets, base, first_image, ev):
         # the draws' stream runs only the draws (the sequential MT19937 stream);
         # the finishing kernels go with the pool, which needs their output
         with torch.cuda.stream(s_rng):
-            s_rng.wait_event(prep_ready[j])
+            # every event record / wait on this stream is a packet the hardware queue
+            # retires between two samplers (~4-6 us each, profiles/r4_experiments.md):
+            # one wait (prop_ready follows prep_ready on the same stream) and one
+            # timing record per step
             if args.rng_waits == "front":  # both samplers back to back (the prepares run ahead)
                 s_rng.wait_event(prop_ready)
-            if timed:
-                d = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-                d[0].record(s_rng)
+            else:
+                s_rng.wait_event(prep_ready[j])
             targets.anchor_targets_draw(plan, rng=rng)
-            at_drawn = torch.cuda.Event()
-            at_drawn.record(s_rng)
             if args.rng_waits != "front":
                 s_rng.wait_event(prop_ready)
             s_cnt = targets.proposal_targets_draw(pplan, rng=rng, count=pt_out[j][3])
-            pt_drawn = torch.cuda.Event()
+            pt_drawn = torch.cuda.Event(enable_timing=timed)
             pt_drawn.record(s_rng)
             if timed:
-                d[1].record(s_rng)
-                ev["draw"].append((d[0], d[1]))
+                ev["draw"].append(pt_drawn)
         with torch.cuda.stream(s_pool):
-            s_pool.wait_event(at_drawn)
+            # the AnchorTarget finish waits for both draws (one event on the draws'
+            # stream): it only has to precede the pool, which needs the second anyway
+            s_pool.wait_event(pt_drawn)
             reg_t, lab = targets.anchor_targets_finish(plan, out=at_out[j])
             sample_ev[j].record(s_pool)
             sample_done[j] = sample_ev[j]   # at_ws[j] free for step k+2's prepare
-            s_pool.wait_event(pt_drawn)
             s_roi, s_reg, s_lab = targets.proposal_targets_finish(pplan, s_cnt, out=pt_out[j][:3])
             sample_rois = s_roi.float().view(-1, 4)          # train.py:86,102,107
             pt_ev[j].record(s_pool)
@@ -760,13 +760,14 @@ def main():
         # the training step's critical path is not an HBM kernel: the target
         # creators' draws walk numpy's sequential MT19937 stream, one workgroup
         # each (at_sample_kernel, then pt_sample_kernel) on the draws' stream
-        draw_us = float(np.mean([a.elapsed_time(b) for a, b in ev["draw"]])) * 1e3
+        dr = ev["draw"]  # the draws' stream period: one record per step after the second sampler
+        draw_us = float(np.mean([a.elapsed_time(b) for a, b in zip(dr[:-1], dr[1:])])) * 1e3
         pool_roof["fwd_event_interval_us_in_pipeline"] = fwd_ms * 1e3
         roof = {"bound": "latency", "kernel": "at_sample_kernel", "unit": "us/step",
                 "achieved": draw_us, "peak": None, "frac": None, "traffic": None,
-                "basis": "the two draws (at_sample_kernel + pt_sample_kernel, one 1024-thread workgroup "
-                         "each, sequential MT19937 stream) per step on the draws' stream, HIP events; "
-                         "latency-bound, so no HBM / MFMA peak applies",
+                "basis": "the draws' stream period (at_sample_kernel + pt_sample_kernel, one 1024-thread "
+                         "workgroup each, sequential MT19937 stream, + the stream's wait / record packets) "
+                         "between consecutive steps, HIP events; latency-bound, so no HBM / MFMA peak applies",
                 "draws_share_of_step": draw_us / (ms_step * 1e3),
                 "roi_pool_bwd": pool_roof}
         pool_roof = roof
