@@ -26,12 +26,15 @@ constexpr int kPathRing = 2;     // roi_pool_bwd: the RoI-at-a-time ring kernel 
 constexpr int kPathHybrid = 1;   // propose: fused per image + chip-wide first-chunk mask
 constexpr int kPathLazy = 2;     // propose: fused per image, lazy NMS from the first chunk on
 constexpr int kPathWide = 3;     // propose: chip-wide sort + bitmask NMS
+constexpr int kPathWalk = 1;     // sampler: one workgroup walks the MT19937 stream (auto)
+constexpr int kPathChip = 2;     // sampler: chip-wide chunk functions + a one-wave chain (draws.h)
 struct PathCfg {
     int roi_fwd = kPathAuto;
     int roi_bwd = kPathAuto;
     int propose = kPathAuto;
     int roi_split = 0;  // RoI shares per (image, channel group); 0 = auto
     int roi_cg = 0;     // channels per RoIPool workgroup (4 / 8 / 16); 0 = auto
+    int sampler = kPathAuto;
 };
 const PathCfg& path_cfg();
 
