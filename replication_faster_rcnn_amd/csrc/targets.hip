@@ -404,23 +404,23 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
                     const float pa = (static_cast<float>(i_loc) + 1.0f) *
                                      __builtin_amdgcn_rcpf(static_cast<float>(mask_for(static_cast<uint32_t>(i_loc))) + 1.0f);
                     const int ig0 = i_loc - static_cast<int>(static_cast<float>(lane) * pa);
-                    uint64_t ac = __ballot(ig0 >= 1 && (wc & mask_for(static_cast<uint32_t>(ig0))) <=
+                    uint64_t ac = __builtin_amdgcn_ballot_w64(ig0 >= 1 && (wc & mask_for(static_cast<uint32_t>(ig0))) <=
                                                          static_cast<uint32_t>(ig0));
                     int ilc;
                     uint32_t mc;
-                    bool ak;
                     for (;;) {
                         const int below = static_cast<int>(__builtin_amdgcn_mbcnt_hi(
                             static_cast<uint32_t>(ac >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(ac), 0u)));
                         ilc = i_loc - below;
-                        const bool valid = ilc >= 1;
-                        mc = mask_for(static_cast<uint32_t>(valid ? ilc : 1));
-                        ak = valid && (wc & mc) <= static_cast<uint32_t>(ilc);
-                        const uint64_t nac = __ballot(ak);
+                        // accepted iff ilc >= 1 and (w & mask) <= ilc, i.e.
+                        // max(w & mask, 1) <= max(ilc, 0): one compare feeds the ballot
+                        const uint32_t ip = static_cast<uint32_t>(ilc > 0 ? ilc : 0);
+                        mc = mask_for(ip);
+                        const uint64_t nac = __builtin_amdgcn_ballot_w64(max(wc & mc, 1u) <= ip);
                         if (nac == ac) break;
                         ac = nac;
                     }
-                    if (ak && ilc >= rec_lo) J[ilc - rec_lo] = static_cast<int>(wc & mc);
+                    if (((ac >> lane) & 1ull) && ilc >= rec_lo) J[ilc - rec_lo] = static_cast<int>(wc & mc);
                     const int cntc = __popcll(ac);
                     used = i_loc - cntc < 1 ? 64 * c + 64 - __clzll(ac) : 64 * (c + 1);
                     i_loc -= cntc;
@@ -463,7 +463,7 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
 #pragma unroll
         for (int sc = 0; sc < kSubc; ++sc) {
             const int ig = i_cur - base - static_cast<int>(static_cast<float>(sc * 64 + lane) * p_acc);
-            acc[sc] = __ballot(ig >= 1 && (w[sc] & mask_for(static_cast<uint32_t>(ig))) <= static_cast<uint32_t>(ig));
+            acc[sc] = __builtin_amdgcn_ballot_w64(ig >= 1 && (w[sc] & mask_for(static_cast<uint32_t>(ig))) <= static_cast<uint32_t>(ig));
         }
         // Round: each unsettled wave solves its words for its assumed base and
         // publishes (count, margins, base): its pattern stays exact for any base in
@@ -494,10 +494,12 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
                             static_cast<uint32_t>(acc[sc] >> 32),
                             __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(acc[sc]), 0u)));
                         il[sc] = i_cur - base - below;
-                        const bool valid = il[sc] >= 1;
-                        m[sc] = mask_for(static_cast<uint32_t>(valid ? il[sc] : 1));
-                        a[sc] = valid && (w[sc] & m[sc]) <= static_cast<uint32_t>(il[sc]);
-                        const uint64_t nacc = __ballot(a[sc]);
+                        // accepted iff il >= 1 and (w & mask) <= il, i.e.
+                        // max(w & mask, 1) <= max(il, 0): one compare feeds the ballot
+                        // (the lane's decision is read back from it after the loop)
+                        const uint32_t ip = static_cast<uint32_t>(il[sc] > 0 ? il[sc] : 0);
+                        m[sc] = mask_for(ip);
+                        const uint64_t nacc = __builtin_amdgcn_ballot_w64(max(w[sc] & m[sc], 1u) <= ip);
                         ch |= nacc != acc[sc];
                         acc[sc] = nacc;
                         pre += __popcll(nacc);
@@ -512,7 +514,10 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
             uint32_t dn = 0, up = 0;
             int cnt = 0;
 #pragma unroll
-            for (int sc = 0; sc < kSubc; ++sc) cnt += __popcll(acc[sc]);
+            for (int sc = 0; sc < kSubc; ++sc) {
+                cnt += __popcll(acc[sc]);
+                a[sc] = (acc[sc] >> lane) & 1ull;
+            }
             if (!done) {
                 dn = up = 0x3fffffffu;
 #pragma unroll
@@ -541,7 +546,7 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
             const int incl = row16_scan_add(r.x);  // lanes 0..15: prefix over waves
             const int excl = incl - r.x;
             const int d = excl - r.w;  // exact base - assumed base of wave `lane`
-            const uint64_t bad = __ballot(lane < kWinWaves && (d > r.y || -d > r.z));
+            const uint64_t bad = __builtin_amdgcn_ballot_w64(lane < kWinWaves && (d > r.y || -d > r.z));
             const int first_bad = bad ? __ffsll(static_cast<unsigned long long>(bad)) - 1 : kWinWaves;
             const int my_excl = __builtin_amdgcn_readlane(excl, wid < kWinWaves ? wid : 0);
             if (wid < first_bad) {
