@@ -360,6 +360,26 @@ __device__ __forceinline__ int row16_scan_add(int x) {
     return x;
 }
 
+// Both margins of a wave in one reduction: dn and up (clamped to 16 bits; a
+// clamped margin only makes the check conservative) packed, v_pk_min_u16 over
+// DPP row shifts, the four row minima combined on the scalar unit.
+typedef unsigned short __attribute__((ext_vector_type(2))) u16x2;
+__device__ __forceinline__ uint32_t pk_min16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ void wave_min2(uint32_t& dn, uint32_t& up) {
+    uint32_t x = (min(dn, 0xffffu) << 16) | min(up, 0xffffu);
+    x = pk_min16(x, __builtin_amdgcn_update_dpp(0xffffffffu, x, 0x111, 0xf, 0xf, false));  // row_shr:1
+    x = pk_min16(x, __builtin_amdgcn_update_dpp(0xffffffffu, x, 0x112, 0xf, 0xf, false));  // row_shr:2
+    x = pk_min16(x, __builtin_amdgcn_update_dpp(0xffffffffu, x, 0x114, 0xf, 0xf, false));  // row_shr:4
+    x = pk_min16(x, __builtin_amdgcn_update_dpp(0xffffffffu, x, 0x118, 0xf, 0xf, false));  // row_shr:8
+    const uint32_t r0 = __builtin_amdgcn_readlane(x, 15), r1 = __builtin_amdgcn_readlane(x, 31);
+    const uint32_t r2 = __builtin_amdgcn_readlane(x, 47), r3 = __builtin_amdgcn_readlane(x, 63);
+    dn = min(min(r0 >> 16, r1 >> 16), min(r2 >> 16, r3 >> 16));
+    up = min(min(r0 & 0xffffu, r1 & 0xffffu), min(r2 & 0xffffu, r3 & 0xffffu));
+}
+
 __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -536,8 +556,7 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
                     dn = dns < dn ? dns : dn;
                     up = ups < up ? ups : up;
                 }
-                dn = __ockl_wfred_min_u32(dn);
-                up = __ockl_wfred_min_u32(up);
+                wave_min2(dn, up);
             }
             if (lane == 0 && wid < kWinWaves)
                 S.rec[par][wid] = make_int4(cnt, static_cast<int>(dn), static_cast<int>(up), base);
