@@ -446,7 +446,7 @@ __global__ __launch_bounds__(256) void draw_chunk_kernel(DrawWs w) {
 // chain reads a chunk with three LDS reads issued two chunks ahead.  A state
 // outside them reads the chunk's whole directory from global memory; a chunk
 // without a matching entry is walked serially.
-constexpr int kChainRing = 40;
+constexpr int kChainRing = 32;  // (a power of two: slot = c & 31)
 constexpr int kChainWaves = 16;
 constexpr int kStagers = 12;  // waves off SIMD 0 (wave w runs on SIMD w % 4)
 constexpr int kSlotEnt = 4;
@@ -626,7 +626,7 @@ __global__ __launch_bounds__(kChainWaves * 64) void draw_chain_kernel(uint32_t* 
     unsigned long long nspin = 0, nstall = 0;
     auto wait_seq = [&](int cc) {
         int spin = 0;
-        while (lds_acq(&L.seq[cc % kChainRing]) != cc + 1 && ++spin < (1 << 22)) __builtin_amdgcn_s_sleep(0);
+        while (lds_acq(&L.seq[cc & (kChainRing - 1)]) != cc + 1 && ++spin < (1 << 22)) __builtin_amdgcn_s_sleep(0);
         if (spin >= (1 << 22)) lost = true;
         nspin += spin;
         nstall += spin ? 1 : 0;
@@ -647,52 +647,75 @@ __global__ __launch_bounds__(kChainWaves * 64) void draw_chain_kernel(uint32_t* 
         tB = S.tau[lane];
         xB = S.crs[lane];
     }
-    uint32_t sinv = 0;
     __builtin_amdgcn_s_setprio(3);
-    int sq = nch > 2 ? lds_rlx(&L.seq[2 % kChainRing]) : 0;  // chunk c + 2's slot, read one chunk early
-    for (; !ok && !lost && c < nch; ++c) {
-        // chunk c + 2 into registers while chunk c is resolved
-        uint4 dC = dB, tC = tB, xC = xB;
+    int sq = nch > 2 ? lds_rlx(&L.seq[2]) : 0;  // chunk c + 2's slot, read one chunk early
+    // One step: chunk c + 2's slot into set Z, chunk c resolved from set X
+    // (set Y holds chunk c + 1).  The loop is unrolled three times with the sets
+    // rotating X -> Y -> Z, so no registers move between steps.
+    auto step = [&](uint4& dX, uint4& tX, uint4& xX, uint4& dZ, uint4& tZ, uint4& xZ) {
         if (c + 2 < nch) {
             if (sq != c + 3) wait_seq(c + 2);
-            const ChainSlot& S = L.slot[(c + 2) % kChainRing];
-            dC = S.dir[lane & (kSlotEnt - 1)];
-            tC = S.tau[lane];
-            xC = S.crs[lane];
-            if (c + 3 < nch) sq = lds_rlx(&L.seq[(c + 3) % kChainRing]);
+            const ChainSlot& S = L.slot[(c + 2) & (kChainRing - 1)];
+            dZ = S.dir[lane & (kSlotEnt - 1)];
+            tZ = S.tau[lane];
+            xZ = S.crs[lane];
+            if (c + 3 < nch) sq = lds_rlx(&L.seq[(c + 3) & (kChainRing - 1)]);
         }
-        sinv = lane == (c & 63) ? s : sinv;
-        if ((c & 63) == 63) w.sin[c - 63 + lane] = sinv;
-        const uint64_t hit = __ballot(lane < kSlotEnt && dA.x != kDrawNone && dA.x <= s && s <= dA.y);
+#ifndef FRCNN_DRAW_DBG
+        if (lane == 0) w.sin[c] = s;
+#endif
+        // the entry holding s (lanes >= kSlotEnt mirror 0..3; an empty entry's
+        // s_lo = kDrawNone exceeds every state), then its function of s
+        const uint64_t hit = __builtin_amdgcn_ballot_w64(dX.x <= s && s <= dX.y);
         uint32_t ns;
         if (hit) {
-            const int e = __ffsll(static_cast<unsigned long long>(hit)) - 1;
-            ns = chain_apply(s, __builtin_amdgcn_readlane(dA.z, e), __builtin_amdgcn_readlane(dA.x, e), pick4(tA, e),
-                             pick4(xA, e), lane);
+            const int e = static_cast<int>(__builtin_amdgcn_readfirstlane(__ffsll(static_cast<unsigned long long>(hit)) - 1));
+            const uint32_t kind = __builtin_amdgcn_readlane(dX.z, e);
+            const uint32_t tv = pick4(tX, e), i = s & kIMask;
+            if (kind & kEntCand) {
+                ns = __builtin_amdgcn_readlane(tv, static_cast<int>(i - (__builtin_amdgcn_readlane(dX.x, e) & kIMask)));
+            } else {
+                const uint32_t lo = (mask_for(i) >> 1) + 1u;
+                const uint64_t acc = __builtin_amdgcn_ballot_w64(tv <= i);
+                const uint32_t n = static_cast<uint32_t>(__popcll(acc));
+                if (n - static_cast<uint32_t>(acc >> 63) <= i - lo) {
+                    ns = s - n;  // (k, i - n): i - n >= lo - 1 >= 63
+                } else {  // the (i - lo + 1)-th acceptance leaves the region; the rest from (k, lo - 1)
+                    const uint32_t before = __builtin_amdgcn_mbcnt_hi(
+                        static_cast<uint32_t>(acc >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(acc), 0u));
+                    const uint64_t at = __builtin_amdgcn_ballot_w64(((acc >> lane) & 1ull) && before == i - lo);
+                    ns = __builtin_amdgcn_readlane(pick4(xX, e), __ffsll(static_cast<unsigned long long>(at)) - 1);
+                }
+            }
         } else {
             bool walked = false;
             ns = chain_global(w, c, s, lane, nc, walked);
             ++slow;
             fb += walked ? 1 : 0;
         }
-        s = ns;
-        lds_put(reinterpret_cast<int*>(&L.s_pub), static_cast<int>(s));
-        lds_put(&L.pos, c + 1);
-        dA = dB;
-        tA = tB;
-        xA = xB;
-        dB = dC;
-        tB = tC;
-        xB = xC;
+        s = __builtin_amdgcn_readfirstlane(ns);
+#ifdef FRCNN_DRAW_DBG
+        if ((c & 3) == 3) {
+#else
+        {
+#endif
+            lds_put(reinterpret_cast<int*>(&L.s_pub), static_cast<int>(s));
+            lds_put(&L.pos, c + 1);
+        }
         if (static_cast<int>(s >> kIBits) >= nc) {
             consumed = c * kDrawChunk + static_cast<int>(s & kIMask);
             ok = true;
         }
-    }
-    // c = chunks walked; flush the entering states of the last partial batch
-    if (c > 0 && (c & 63) != 0) {
-        const int b0 = (c - 1) & ~63;
-        if (b0 + lane < c) w.sin[b0 + lane] = sinv;
+        ++c;
+        return ok || lost || c >= nch;
+    };
+    uint4 dC = dA, tC = tA, xC = xA;
+    if (!ok && nch > 0) {
+        for (;;) {
+            if (step(dA, tA, xA, dC, tC, xC)) break;
+            if (step(dB, tB, xB, dA, tA, xA)) break;
+            if (step(dC, tC, xC, dB, tB, xB)) break;
+        }
     }
     lds_rel(&L.stop, 1);
     if (lane == 0) {
