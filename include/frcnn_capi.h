@@ -171,9 +171,10 @@ int frcnn_roi_pool_fwd_head(const float* x, const float* rois, const float* roi_
                             float spatial_scale, int rois_sorted, float* boxes, float* out,
                             int32_t* argmax, void* workspace, size_t ws_bytes, void* stream);
 
-/* The kernel frcnn_roi_pool_fwd_head (head != 0, 16-B aligned rois) or
- * frcnn_roi_pool_fwd (head == 0) launches for this shape on `stream` under the
- * current frcnn_set_path choices, as its template name (e.g.
+/* The kernel frcnn_roi_pool_fwd_head (head == 1: 16-B aligned rois; head == 2:
+ * an unaligned rois pointer, which the head entry point handles as transform +
+ * the plain forward) or frcnn_roi_pool_fwd (head == 0) launches for this shape on
+ * `stream` under the current frcnn_set_path choices, as its template name (e.g.
  * "roi_pool_fwd_pair_kernel<1024, 8, 7, true>"), NUL-terminated in name[len]:
  * the label bench.py and the rocprofv3 records key the dominant kernel on. */
 int frcnn_roi_pool_fwd_kernel(int64_t R, int N, int C, int H, int W, int PH, int PW, int rois_sorted,

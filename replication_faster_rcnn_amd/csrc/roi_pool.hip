@@ -2445,7 +2445,9 @@ extern "C" int frcnn_roi_pool_fwd_kernel(int64_t R, int N, int C, int H, int W, 
                   "frcnn_roi_pool_fwd_kernel: bad shape");
     const FwdChoice ch = choose_fwd(N, C, H, W, PH, PW, rois_sorted != 0, as_stream(stream));
     const int fx = PH == 7 && PW == 7 ? 7 : 0;
-    const char* hb = head ? "true" : "false";
+    // head == 2 (unaligned rois): frcnn_roi_pool_fwd_head transforms and then runs the
+    // plain forward, like the dense-list / generic choices below
+    const char* hb = head == 1 ? "true" : "false";
     int n = 0;
     switch (ch.kind) {
         case kFwdPair: n = snprintf(name, len, "roi_pool_fwd_pair_kernel<1024, %d, %d, %s>", ch.px.cg, fx, hb); break;
