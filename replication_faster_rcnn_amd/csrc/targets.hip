@@ -288,7 +288,10 @@ __device__ unsigned long long g_samp_prof[16];
 #define SPROF_ADD(k, v) do {} while (0)
 #define SPROF_DT(k) do {} while (0)
 #endif
-constexpr int kWinWaves = 12;              // waves that walk a window; the other 4 twist ahead
+#ifndef FRCNN_WIN_WAVES
+#define FRCNN_WIN_WAVES 12
+#endif
+constexpr int kWinWaves = FRCNN_WIN_WAVES;  // waves that walk a window; the others twist ahead
 #ifndef FRCNN_SAMP_SUBC
 #define FRCNN_SAMP_SUBC 1
 #endif
@@ -400,8 +403,8 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
         // others walk the window; the window's barriers publish it
         const bool gen = st.ngen < kRing - 1;
         if (gen && wid >= kWinWaves)
-            mt_twist(S.ring[(st.slot + st.ngen) % kRing], S.ring[(st.slot + st.ngen + 1) % kRing],
-                     tid - kWinWaves * 64);
+            for (int t = tid - kWinWaves * 64; t < kMtN - kMtM; t += (kSampWaves - kWinWaves) * 64)
+                mt_twist(S.ring[(st.slot + st.ngen) % kRing], S.ring[(st.slot + st.ngen + 1) % kRing], t);
         SPROF_ADD(0, 1);
         SPROF_T0();
         if (i_cur < kSeqBelow) {
