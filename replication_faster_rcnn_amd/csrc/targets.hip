@@ -257,6 +257,9 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
 __device__ __forceinline__ uint32_t mask_for(uint32_t v) {
     return v ? 0xffffffffu >> __builtin_clz(v) : 0u;
 }
+// mask_for(max(v, 1)): no zero test (for the walks' decision max(w & mask, 1) <=
+// step, where a step <= 0 rejects whatever the mask)
+__device__ __forceinline__ uint32_t mask_nz(uint32_t v) { return 0xffffffffu >> __builtin_clz(v | 1u); }
 
 // ------------------------------------------------------------ stream walker
 // The sampler kernels run as ONE 1024-thread workgroup: the MT19937 stream is a
@@ -427,8 +430,8 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
                     const float pa = (static_cast<float>(i_loc) + 1.0f) *
                                      __builtin_amdgcn_rcpf(static_cast<float>(mask_for(static_cast<uint32_t>(i_loc))) + 1.0f);
                     const int ig0 = i_loc - static_cast<int>(static_cast<float>(lane) * pa);
-                    uint64_t ac = __builtin_amdgcn_ballot_w64(ig0 >= 1 && (wc & mask_for(static_cast<uint32_t>(ig0))) <=
-                                                         static_cast<uint32_t>(ig0));
+                    const uint32_t ig0p = static_cast<uint32_t>(ig0 > 0 ? ig0 : 0);
+                    uint64_t ac = __builtin_amdgcn_ballot_w64(max(wc & mask_nz(ig0p), 1u) <= ig0p);
                     int ilc;
                     uint32_t mc;
                     for (;;) {
@@ -438,7 +441,7 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
                         // accepted iff ilc >= 1 and (w & mask) <= ilc, i.e.
                         // max(w & mask, 1) <= max(ilc, 0): one compare feeds the ballot
                         const uint32_t ip = static_cast<uint32_t>(ilc > 0 ? ilc : 0);
-                        mc = mask_for(ip);
+                        mc = mask_nz(ip);
                         const uint64_t nac = __builtin_amdgcn_ballot_w64(max(wc & mc, 1u) <= ip);
                         if (nac == ac) break;
                         ac = nac;
@@ -486,7 +489,8 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
 #pragma unroll
         for (int sc = 0; sc < kSubc; ++sc) {
             const int ig = i_cur - base - static_cast<int>(static_cast<float>(sc * 64 + lane) * p_acc);
-            acc[sc] = __builtin_amdgcn_ballot_w64(ig >= 1 && (w[sc] & mask_for(static_cast<uint32_t>(ig))) <= static_cast<uint32_t>(ig));
+            const uint32_t igp = static_cast<uint32_t>(ig > 0 ? ig : 0);
+            acc[sc] = __builtin_amdgcn_ballot_w64(max(w[sc] & mask_nz(igp), 1u) <= igp);
         }
         // Round: each unsettled wave solves its words for its assumed base and
         // publishes (count, margins, base): its pattern stays exact for any base in
@@ -521,7 +525,7 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
                         // max(w & mask, 1) <= max(il, 0): one compare feeds the ballot
                         // (the lane's decision is read back from it after the loop)
                         const uint32_t ip = static_cast<uint32_t>(il[sc] > 0 ? il[sc] : 0);
-                        m[sc] = mask_for(ip);
+                        m[sc] = mask_nz(ip);
                         const uint64_t nacc = __builtin_amdgcn_ballot_w64(max(w[sc] & m[sc], 1u) <= ip);
                         ch |= nacc != acc[sc];
                         acc[sc] = nacc;
