@@ -355,6 +355,16 @@ __device__ __forceinline__ void stream_store(const WalkLds& S, const Stream& st,
     if (threadIdx.x == 0) rng[kMtN] = static_cast<uint32_t>(st.off);
 }
 
+// Word `off` past the stream position: the ring's blocks are contiguous in
+// LDS, so the word sits at (slot * 624 + pos + off) modulo the ring (pos + off
+// < 624 + kWin keeps the sum below twice the ring: one conditional subtract).
+static_assert(kWin <= kRing * kMtN, "ring_word: one conditional subtract must wrap any window word");
+__device__ __forceinline__ uint32_t ring_word(const WalkLds& S, const Stream& st, int off) {
+    int f = st.slot * kMtN + st.off + off;
+    f -= f >= kRing * kMtN ? kRing * kMtN : 0;
+    return (&S.ring[0][0])[f];
+}
+
 // Fisher-Yates steps i = i_hi .. 1 of one choice() call on the stream; for
 // steps i >= rec_lo, J[i - rec_lo] = j.  Block-uniform; ends with a barrier.
 // Inclusive prefix sum over each row of 16 lanes (DPP row shifts).
@@ -416,11 +426,7 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
             // chunks in order, each solved exactly on the known step.
             if (wid == 0) {
                 int i_loc = i_cur, used = 0;
-                auto word = [&](int c) {  // chunk c's word of this lane (raw)
-                    const int gc = st.off + 64 * c + lane;
-                    const int bc = gc / kMtN;
-                    return S.ring[(st.slot + bc) % kRing][gc - bc * kMtN];
-                };
+                auto word = [&](int c) { return ring_word(S, st, 64 * c + lane); };  // chunk c's word (raw)
                 uint32_t wn = word(0);  // the next chunk's word is read during this one's fixed point
                 for (int c = 0; c < kWinChunks && i_loc >= 1; ++c) {
                     const uint32_t wc = mt_temper(wn);
@@ -477,9 +483,7 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
         uint32_t w[kSubc];
 #pragma unroll
         for (int sc = 0; sc < kSubc; ++sc) {
-            const int g = st.off + (wid < kWinWaves ? (wid * kSubc + sc) * 64 + lane : 0);
-            const int blk = g / kMtN;
-            w[sc] = mt_temper(S.ring[(st.slot + blk) % kRing][g - blk * kMtN]);
+            w[sc] = mt_temper(ring_word(S, st, wid < kWinWaves ? (wid * kSubc + sc) * 64 + lane : 0));
         }
         const float p_acc = (static_cast<float>(i_cur) + 1.0f) *
                             __builtin_amdgcn_rcpf(static_cast<float>(mask_for(static_cast<uint32_t>(i_cur))) + 1.0f);
