@@ -307,6 +307,7 @@ constexpr int kRing = (kMtN + kWin - 1) / kMtN + 2;
 #define FRCNN_SEQ_BELOW 1024
 #endif
 constexpr int kSeqBelow = FRCNN_SEQ_BELOW;  // steps below which one wave walks the window
+static_assert(kSeqBelow <= (1 << 15), "the sequential walk's 16-bit fixed-point guess");
 
 struct Stream {  // block-uniform: every thread tracks the same values
     int slot;    // ring slot of the block numpy's key[] holds
@@ -315,7 +316,8 @@ struct Stream {  // block-uniform: every thread tracks the same values
 };
 
 struct WalkLds {
-    uint32_t ring[kRing][kMtN];
+    uint32_t ring[kRing][kMtN];   // raw state blocks (the twist's input, the state handed back)
+    uint32_t tring[kRing][kMtN];  // the same words tempered (what the walkers read)
     int4 rec[2][kSampWaves];  // per wave, by round parity: (accepted words, margin down, margin up, base)
     int last[kSampWaves];     // per wave: highest accepted word + 1
 };
@@ -328,23 +330,34 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
 // numpy's mt19937_gen: nw = the state block after old (words i < 227 read
 // old[i + 397], later words the new word 227 before them; word 623 reads the
 // new word 0).  Threads t = 0..226 of the caller's group do the work.
-__device__ __forceinline__ void mt_twist(const uint32_t* __restrict__ old, uint32_t* __restrict__ nw, int t) {
+__device__ __forceinline__ void mt_twist(const uint32_t* __restrict__ old, uint32_t* __restrict__ nw,
+                                         uint32_t* __restrict__ tw, int t) {
     if (t < kMtN - kMtM) {
         const uint32_t a = old[t + kMtM] ^ mt_mix(old[t], old[t + 1]);
         const uint32_t b = a ^ mt_mix(old[t + 227], old[t + 228]);
         nw[t] = a;
         nw[t + 227] = b;
+        tw[t] = mt_temper(a);
+        tw[t + 227] = mt_temper(b);
         if (t + 454 < kMtN - 1) {
-            nw[t + 454] = b ^ mt_mix(old[t + 454], old[t + 455]);
+            const uint32_t c = b ^ mt_mix(old[t + 454], old[t + 455]);
+            nw[t + 454] = c;
+            tw[t + 454] = mt_temper(c);
         } else if (t + 454 == kMtN - 1) {
             const uint32_t n0 = old[kMtM] ^ mt_mix(old[0], old[1]);
-            nw[kMtN - 1] = b ^ mt_mix(old[kMtN - 1], n0);
+            const uint32_t c = b ^ mt_mix(old[kMtN - 1], n0);
+            nw[kMtN - 1] = c;
+            tw[kMtN - 1] = mt_temper(c);
         }
     }
 }
 
 __device__ __forceinline__ void stream_load(WalkLds& S, Stream& st, const uint32_t* __restrict__ rng) {
-    for (int i = threadIdx.x; i < kMtN; i += kSampThreads) S.ring[0][i] = rng[i];
+    for (int i = threadIdx.x; i < kMtN; i += kSampThreads) {
+        const uint32_t v = rng[i];
+        S.ring[0][i] = v;
+        S.tring[0][i] = mt_temper(v);
+    }
     st.slot = 0;
     st.off = static_cast<int>(rng[kMtN]);
     st.ngen = 0;
@@ -355,14 +368,14 @@ __device__ __forceinline__ void stream_store(const WalkLds& S, const Stream& st,
     if (threadIdx.x == 0) rng[kMtN] = static_cast<uint32_t>(st.off);
 }
 
-// Word `off` past the stream position: the ring's blocks are contiguous in
+// Tempered word `off` past the stream position: the ring's blocks are contiguous in
 // LDS, so the word sits at (slot * 624 + pos + off) modulo the ring (pos + off
 // < 624 + kWin keeps the sum below twice the ring: one conditional subtract).
 static_assert(kWin <= kRing * kMtN, "ring_word: one conditional subtract must wrap any window word");
 __device__ __forceinline__ uint32_t ring_word(const WalkLds& S, const Stream& st, int off) {
     int f = st.slot * kMtN + st.off + off;
     f -= f >= kRing * kMtN ? kRing * kMtN : 0;
-    return (&S.ring[0][0])[f];
+    return (&S.tring[0][0])[f];
 }
 
 // Fisher-Yates steps i = i_hi .. 1 of one choice() call on the stream; for
@@ -405,7 +418,8 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
         {
             SPROF_T0();
             while (st.ngen < need) {  // (only when the twisting waves fell behind)
-                mt_twist(S.ring[(st.slot + st.ngen) % kRing], S.ring[(st.slot + st.ngen + 1) % kRing], tid);
+                mt_twist(S.ring[(st.slot + st.ngen) % kRing], S.ring[(st.slot + st.ngen + 1) % kRing],
+                         S.tring[(st.slot + st.ngen + 1) % kRing], tid);
                 __syncthreads();
                 ++st.ngen;
                 SPROF_ADD(1, 1);
@@ -417,7 +431,8 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
         const bool gen = st.ngen < kRing - 1;
         if (gen && wid >= kWinWaves)
             for (int t = tid - kWinWaves * 64; t < kMtN - kMtM; t += (kSampWaves - kWinWaves) * 64)
-                mt_twist(S.ring[(st.slot + st.ngen) % kRing], S.ring[(st.slot + st.ngen + 1) % kRing], t);
+                mt_twist(S.ring[(st.slot + st.ngen) % kRing], S.ring[(st.slot + st.ngen + 1) % kRing],
+                         S.tring[(st.slot + st.ngen + 1) % kRing], t);
         SPROF_ADD(0, 1);
         SPROF_T0();
         if (i_cur < kSeqBelow) {
@@ -426,16 +441,17 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
             // chunks in order, each solved exactly on the known step.
             if (wid == 0) {
                 int i_loc = i_cur, used = 0;
-                auto word = [&](int c) { return ring_word(S, st, 64 * c + lane); };  // chunk c's word (raw)
+                auto word = [&](int c) { return ring_word(S, st, 64 * c + lane); };  // chunk c's word
                 uint32_t wn = word(0);  // the next chunk's word is read during this one's fixed point
                 for (int c = 0; c < kWinChunks && i_loc >= 1; ++c) {
-                    const uint32_t wc = mt_temper(wn);
+                    const uint32_t wc = wn;
                     if (c + 1 < kWinChunks) wn = word(c + 1);
-                    // (a guess: any start reaches the same fixed point, so the
-                    // approximate reciprocal, not the IEEE division the build flags make '/')
-                    const float pa = (static_cast<float>(i_loc) + 1.0f) *
-                                     __builtin_amdgcn_rcpf(static_cast<float>(mask_for(static_cast<uint32_t>(i_loc))) + 1.0f);
-                    const int ig0 = i_loc - static_cast<int>(static_cast<float>(lane) * pa);
+                    // (a guess: any start reaches the same fixed point) the expected
+                    // acceptances before the lane, (i + 1) / 2^bits(i) per word, in
+                    // 16-bit fixed point (i < kSeqBelow here)
+                    const uint32_t pa16 = (static_cast<uint32_t>(i_loc + 1) << 16) >>
+                                          (32 - __builtin_clz(static_cast<uint32_t>(i_loc)));
+                    const int ig0 = i_loc - static_cast<int>((static_cast<uint32_t>(lane) * pa16) >> 16);
                     const uint32_t ig0p = static_cast<uint32_t>(ig0 > 0 ? ig0 : 0);
                     uint64_t ac = __builtin_amdgcn_ballot_w64(max(wc & mask_nz(ig0p), 1u) <= ig0p);
                     int ilc;
@@ -483,7 +499,7 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
         uint32_t w[kSubc];
 #pragma unroll
         for (int sc = 0; sc < kSubc; ++sc) {
-            w[sc] = mt_temper(ring_word(S, st, wid < kWinWaves ? (wid * kSubc + sc) * 64 + lane : 0));
+            w[sc] = ring_word(S, st, wid < kWinWaves ? (wid * kSubc + sc) * 64 + lane : 0);
         }
         const float p_acc = (static_cast<float>(i_cur) + 1.0f) *
                             __builtin_amdgcn_rcpf(static_cast<float>(mask_for(static_cast<uint32_t>(i_cur))) + 1.0f);
