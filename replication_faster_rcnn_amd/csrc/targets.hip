@@ -468,7 +468,8 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
                         if (nac == ac) break;
                         ac = nac;
                     }
-                    if (((ac >> lane) & 1ull) && ilc >= rec_lo) J[ilc - rec_lo] = static_cast<int>(wc & mc);
+                    if (i_loc >= rec_lo && ((ac >> lane) & 1ull) && ilc >= rec_lo)  // (i_loc: wave-uniform skip)
+                        J[ilc - rec_lo] = static_cast<int>(wc & mc);
                     const int cntc = __popcll(ac);
                     used = i_loc - cntc < 1 ? 64 * c + 64 - __clzll(ac) : 64 * (c + 1);
                     i_loc -= cntc;
@@ -611,9 +612,11 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
             if (first_bad == kWinWaves) break;
         }
         SPROF_DT(4);
+        if (i_cur - base >= rec_lo) {  // (the wave's first step: a wave-uniform skip)
 #pragma unroll
-        for (int sc = 0; sc < kSubc; ++sc)
-            if (a[sc] && il[sc] >= rec_lo) J[il[sc] - rec_lo] = static_cast<int>(w[sc] & m[sc]);
+            for (int sc = 0; sc < kSubc; ++sc)
+                if (a[sc] && il[sc] >= rec_lo) J[il[sc] - rec_lo] = static_cast<int>(w[sc] & m[sc]);
+        }
         int consumed = kWin;
         if (i_cur - total < 1) {  // the call ends inside this window
             if (lane == 0 && wid < kWinWaves) {
