@@ -741,8 +741,17 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
                 int32_t* ap = argmax + o;
 #pragma unroll
                 for (int c = 0; c < CG; ++c) {
+#ifndef FRCNN_WAVE_TEMPORAL
+                    // non-temporal: the outputs are read only by the next layer, so
+                    // they need not displace the features and the next steps'
+                    // proposal data from the L2 / Infinity Cache (cfg2 driver
+                    // command 98.5-99.1k -> 103.2-103.6k images/s, round 4)
+                    __builtin_nontemporal_store(mv[c], op + c * PHW);
+                    __builtin_nontemporal_store(mi[c], ap + c * PHW);
+#else
                     op[c * PHW] = mv[c];
                     ap[c * PHW] = mi[c];
+#endif
                 }
             }
             k = __builtin_amdgcn_readfirstlane(kn);
