@@ -103,6 +103,8 @@ def parse():
     ap.add_argument("--dist-backend", default="auto", choices=("auto", "nccl", "gloo"),
                     help="auto: nccl (RCCL over xGMI) when every rank has a GPU of its own, "
                          "gloo (host copies) when ranks share one")
+    ap.add_argument("--roi-store", default="auto", choices=("auto", "temporal", "nt"),
+                    help="RoIPool forward output stores (frcnn_set_path roi_pool_fwd_store): nt = non-temporal")
     ap.add_argument("--roi-cg", default="auto",
                     help="channels per RoIPool forward workgroup (frcnn_set_path roi_pool_cg): auto | 4 | 8 | 16")
     ap.add_argument("--roi-path", default="auto",
@@ -656,7 +658,7 @@ def main():
     dev = torch.device("cuda", dev_index)
     from replication_faster_rcnn_amd import _lib
     from replication_faster_rcnn_amd import anchors as A
-    for op, v in (("roi_pool_cg", args.roi_cg), ("roi_pool_split", args.roi_split),
+    for op, v in (("roi_pool_cg", args.roi_cg), ("roi_pool_split", args.roi_split), ("roi_pool_fwd_store", args.roi_store),
                   ("roi_pool_fwd", args.roi_path), ("propose", args.propose_path)):
         if v != "auto":
             _lib.set_path(op, v)
@@ -795,7 +797,7 @@ def main():
                    "parallelism": f"dp{world} (per-image sharding)", "streams": args.streams,
                    "prop_streams": args.prop_streams if (args.streams == 2 and not train) else 1,
                    "pool_on": args.pool_on if (args.streams == 2 and not train) else None,
-                   "host_io": bool(args.host_io), "rng_waits": args.rng_waits, "roi_path": args.roi_path, "roi_cg": args.roi_cg, "roi_split": args.roi_split,
+                   "host_io": bool(args.host_io), "rng_waits": args.rng_waits, "roi_path": args.roi_path, "roi_cg": args.roi_cg, "roi_split": args.roi_split, "roi_store": args.roi_store,
                    "prop_cus": args.prop_cus if (args.streams == 2 and not train) else 0,
                    "propose_path": args.propose_path,
                    "collective": (None if world == 1 else

@@ -62,6 +62,8 @@ int frcnn_probe_hw_ids(uint32_t* out, int nblocks, int spin, void* stream);
  *   "propose"        : "auto" | "hybrid" | "lazy" (fused per image) | "wide" (chip-wide bitmask)
  *   "roi_pool_split" : "auto" | "1".."64" (RoI shares per image and channel group)
  *   "roi_pool_cg"    : "auto" | "4" | "8" | "16" (channels per RoIPool forward workgroup)
+ *   "roi_pool_fwd_store": "auto" = "temporal" | "nt" (the wave forward's output stores
+ *                      non-temporal: better beside concurrent kernels at cfg2, worse alone)
  *   "sampler"        : "auto" | "walk" (one workgroup walks the MT19937 stream; the auto
  *                      choice) | "chip" (chip-wide chunk functions + a one-wave chain,
  *                      csrc/draws.h; the target creators' _draw / _sample entry points)

@@ -82,6 +82,8 @@ extern "C" int frcnn_set_path(const char* op, const char* path) {
         g_path.propose = aut ? kPathAuto : is(path, "hybrid") ? kPathHybrid
                                          : is(path, "lazy")   ? kPathLazy
                                                               : kPathWide;
+    } else if (is(op, "roi_pool_fwd_store") && (aut || is(path, "temporal") || is(path, "nt"))) {
+        g_path.roi_store = is(path, "nt") ? 1 : 0;
     } else if (is(op, "sampler") && (aut || is(path, "walk") || is(path, "chip"))) {
         g_path.sampler = aut ? kPathAuto : is(path, "walk") ? kPathWalk : kPathChip;
     } else if (is(op, "roi_pool_split")) {

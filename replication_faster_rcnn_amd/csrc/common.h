@@ -35,6 +35,7 @@ struct PathCfg {
     int roi_split = 0;  // RoI shares per (image, channel group); 0 = auto
     int roi_cg = 0;     // channels per RoIPool workgroup (4 / 8 / 16); 0 = auto
     int sampler = kPathAuto;
+    int roi_store = 0;  // RoIPool forward (wave kernel) output stores: 0 temporal (auto), 1 non-temporal
 };
 const PathCfg& path_cfg();
 

@@ -585,7 +585,7 @@ __device__ __forceinline__ const float4* tile_px(const float4* q4, int p) {
 // shape per image or per RoI block -- are slower: DESIGN.md §3.)
 // FIX = PH = PW known at compile time (the 7x7 head): the 2 x CG output
 // stores of a RoI take immediate offsets from one base address.
-template <int NT, int CG, int FIX, bool HEAD>
+template <int NT, int CG, int FIX, bool HEAD, bool NTS = false>
 __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
     const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W, int PH_, int PW_,
     float ss, float* __restrict__ out, int32_t* __restrict__ argmax, int geo_cap, HeadArgs hd) {
@@ -739,19 +739,24 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
                 const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
                 float* op = out + o;
                 int32_t* ap = argmax + o;
+                if constexpr (NTS) {  // (a template choice: a runtime branch gets its stores
+                                      // merged with the temporal ones, hint dropped)
+                    // non-temporal (frcnn_set_path("roi_pool_fwd_store", "nt")): the
+                    // outputs then do not displace what concurrent kernels cache --
+                    // the cfg2 pipeline gains 5 %, but alone every config loses and
+                    // cfg1 / cfg3 / cfg4 lose 5-12 % (profiles/r4_experiments.md),
+                    // and a real head reads the outputs next, so temporal is the default
 #pragma unroll
-                for (int c = 0; c < CG; ++c) {
-#ifndef FRCNN_WAVE_TEMPORAL
-                    // non-temporal: the outputs are read only by the next layer, so
-                    // they need not displace the features and the next steps'
-                    // proposal data from the L2 / Infinity Cache (cfg2 driver
-                    // command 98.5-99.1k -> 103.2-103.6k images/s, round 4)
-                    __builtin_nontemporal_store(mv[c], op + c * PHW);
-                    __builtin_nontemporal_store(mi[c], ap + c * PHW);
-#else
-                    op[c * PHW] = mv[c];
-                    ap[c * PHW] = mi[c];
-#endif
+                    for (int c = 0; c < CG; ++c) {
+                        __builtin_nontemporal_store(mv[c], op + c * PHW);
+                        __builtin_nontemporal_store(mi[c], ap + c * PHW);
+                    }
+                } else {
+#pragma unroll
+                    for (int c = 0; c < CG; ++c) {
+                        op[c * PHW] = mv[c];
+                        ap[c * PHW] = mi[c];
+                    }
                 }
             }
             k = __builtin_amdgcn_readfirstlane(kn);
@@ -2188,9 +2193,15 @@ int px_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, in
               int PH, int PW, float ss, float* out, int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
     const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(pl.split), static_cast<unsigned>(N + 1));
     const bool fix7 = PH == 7 && PW == 7;
-#define FRCNN_PX(CG, FX)                                                                                    \
-    hipLaunchKernelGGL((roi_pool_fwd_wave_kernel<1024, CG, FX, HEAD>), grid, dim3(1024), pl.lds, st, x, rois, \
-                       static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd)
+#define FRCNN_PX(CG, FX)                                                                                         \
+    do {                                                                                                         \
+        if (path_cfg().roi_store)                                                                                \
+            hipLaunchKernelGGL((roi_pool_fwd_wave_kernel<1024, CG, FX, HEAD, true>), grid, dim3(1024), pl.lds, st, \
+                               x, rois, static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd);  \
+        else                                                                                                     \
+            hipLaunchKernelGGL((roi_pool_fwd_wave_kernel<1024, CG, FX, HEAD>), grid, dim3(1024), pl.lds, st, x,    \
+                               rois, static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd);    \
+    } while (0)
     if (pl.cg == 16) {
         if (fix7) FRCNN_PX(16, 7); else FRCNN_PX(16, 0);
     } else if (pl.cg == 8) {
@@ -2461,7 +2472,10 @@ extern "C" int frcnn_roi_pool_fwd_kernel(int64_t R, int N, int C, int H, int W, 
     switch (ch.kind) {
         case kFwdPair: n = snprintf(name, len, "roi_pool_fwd_pair_kernel<1024, %d, %d, %s>", ch.px.cg, fx, hb); break;
         case kFwdKey: n = snprintf(name, len, "roi_pool_fwd_key_kernel<%d, %d, %d, %s>", kKeyNT, ch.px.cg, fx, hb); break;
-        case kFwdWave: n = snprintf(name, len, "roi_pool_fwd_wave_kernel<1024, %d, %d, %s>", ch.px.cg, fx, hb); break;
+        case kFwdWave:
+            n = snprintf(name, len, "roi_pool_fwd_wave_kernel<1024, %d, %d, %s%s>", ch.px.cg, fx, hb,
+                         path_cfg().roi_store ? ", true" : "");
+            break;
         case kFwdDense:
             n = snprintf(name, len, "roi_pool_fwd_dense_kernel<1024, %d, %d, %s, false>", ch.dn.cg, fx, hb);
             break;

@@ -290,6 +290,23 @@ def test_roi_pool_special_values(fpath, sorted_):
     assert np.array_equal(out.cpu().numpy().view(np.uint32), oo.view(np.uint32))
 
 
+def test_roi_pool_nontemporal_stores():
+    """The wave forward with non-temporal output stores (roi_pool_fwd_store nt):
+    the same bits as the oracle, special values included."""
+    r = np.random.default_rng(7)
+    x = _special_x(r)
+    N = x.shape[0]
+    rois = np.array([[b, x1, y1, x1 + w, y1 + h] for b in range(N) for (x1, y1, w, h) in
+                     [(0, 0, 13, 11), (1, 2, 5, 3), (3, 3, 0, 0), (2, 1, 9, 9), (-3, -2, 20, 20)]], np.float32)
+    with _lib.kernel_path("roi_pool_fwd", "wave"), _lib.kernel_path("roi_pool_fwd_store", "nt"):
+        out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7,
+                                           rois_sorted=True)
+        assert _lib.roi_pool_fwd_kernel(len(rois), N, x.shape[1], x.shape[2], x.shape[3]).endswith(", true>")
+    oo, oa = orc.roi_pool_forward(x, rois, 7)
+    assert np.array_equal(am.cpu().numpy(), oa)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), oo.view(np.uint32))
+
+
 @pytest.mark.parametrize("fpath,sorted_", FWD_PATHS)
 def test_roi_pool_paths_random(fpath, sorted_):
     """Every forward path, cfg2-like random RoIs with plenty of ties, bit-exact vs the oracle."""
