@@ -1857,9 +1857,9 @@ constexpr int kBwdXRow = 80;  // leader kernel: exchange-row entries per wave (i
 // ds_write_b64, eight ds_read_b64 at immediate offsets, conflict free) -- a
 // third of the LDS cycles of twelve ds_bpermute.  RoIs flagged by the prep kernel (tiny
 // windows overlapping beyond the neighbours) rank their bins from the full
-// overlap mask and apply in rounds, as the ring kernel.  D RoIs per step: the
-// exchanges of the D RoIs are issued before their read-add-writes go to the
-// plane in RoI order.
+// overlap mask and apply in rounds, as the ring kernel.  D RoIs per step, two
+// per exchange; each pair's read-add-writes go to the plane in RoI order behind
+// the next pair's exchange.
 template <int D, int PWT>
 __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
     const float* __restrict__ grad, const int32_t* __restrict__ argmax,
@@ -1903,10 +1903,19 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
         const uint32_t mb = static_cast<uint32_t>(R) * PHW;
         const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(grad), 0, gb, 0x00020000);
         const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(argmax), 0, gb, 0x00020000);
-        // overlap masks are read only for flagged RoIs: the others load through
-        // a descriptor with no records (the load returns 0, no memory access)
+        // overlap masks are read only for flagged RoIs, behind a scalar branch on the
+        // (wave-uniform) list entry: a masked-off load through an empty descriptor
+        // still cost its address cycles (cfg5 op 93.3 -> 90.4 us, profiles/r4_experiments.md)
         const auto rs_m = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(cmask), 0, mb * 8, 0x00020000);
-        const auto rs_0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(cmask), 0, 0, 0x00020000);
+        auto mask_load = [&](int e, uint32_t& clo, uint32_t& chi) {
+            const uint32_t sm8 = static_cast<uint32_t>(e) * (PHW * 8);
+            clo = chi = 0;
+            if (e < 0) {
+                const auto m = __builtin_amdgcn_raw_buffer_load_b64(rs_m, kl * 8, sm8, 0);
+                clo = m[0];
+                chi = m[1];
+            }
+        };
         const uint32_t cpb = static_cast<uint32_t>(c) * PHW * 4;
         const uint32_t rpb = static_cast<uint32_t>(C) * PHW * 4;
         int am_r[D], fl_r[D];
@@ -1923,12 +1932,9 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
             const int e = lst[d];
             fl_r[d] = e < 0;
             const uint32_t so = static_cast<uint32_t>(e) * rpb + cpb;
-            const uint32_t sm8 = static_cast<uint32_t>(e) * (PHW * 8);
             am_r[d] = __builtin_amdgcn_raw_buffer_load_b32(rs_a, kl * 4, so, 0);
             g_r[d] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g, kl * 4, so, 0));
-            const auto m = __builtin_amdgcn_raw_buffer_load_b64(e < 0 ? rs_m : rs_0, kl * 8, sm8, 0);
-            cl_r[d] = m[0];
-            ch_r[d] = m[1];
+            mask_load(e, cl_r[d], ch_r[d]);
             asm volatile("" ::: "memory");
         }
         unsigned long long tp[3] = {0, 0, 0};
@@ -1954,21 +1960,15 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
                 g_r[d] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g, kl * 4, so, 0));
             }
             const unsigned long long p1 = BPROF_T();
-            // neighbour exchanges, two slots per LDS round trip (each slot its
-            // own row; plane-independent; LDS runs a wave's accesses in order,
-            // so a row's next write follows its reads); flagged RoIs rank
-            // their bins from the overlap mask, then the mask slot is refilled
+            // The exchange of slot pair k + 1 is issued before the read-add-writes of pair k
+            // and waited for after them: LDS serves a wave in order, so its reads ride in the
+            // shadow of the plane round trips (one exchange round trip per step instead of
+            // D / 2).  The exchange's outputs are tied to the wait by "+v" operands.
             static_assert(D % 2 == 0, "slots are exchanged in pairs");
             auto lo = [](uint64_t q) { return static_cast<int>(static_cast<uint32_t>(q)); };
             auto hi = [](uint64_t q) { return __builtin_bit_cast(float, static_cast<uint32_t>(q >> 32)); };
-#pragma unroll
-            for (int d0 = 0; d0 < D; d0 += 2) {
-                // per slot: one ds_write_b64 of this lane's pair, eight
-                // ds_read_b64 of the neighbours' at immediate offsets; one wait
-                // for both.  In asm, since other lanes' words are invisible to
-                // the compiler's ordering.  (64-bit scalars, not int2 vectors,
-                // as operands: a vector output's high half was read as its low.)
-                uint64_t q[2][8];
+            uint64_t q[2][8];
+            auto x_issue = [&](int d0) {
                 const uint64_t m0 = static_cast<uint32_t>(am[d0]) |
                                     (static_cast<uint64_t>(__builtin_bit_cast(uint32_t, g[d0])) << 32);
                 const uint64_t m1 = static_cast<uint32_t>(am[d0 + 1]) |
@@ -1991,8 +1991,7 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
                     "ds_read_b64 %12, %17 offset:%c24\n\t"
                     "ds_read_b64 %13, %17 offset:%c25\n\t"
                     "ds_read_b64 %14, %17 offset:%c26\n\t"
-                    "ds_read_b64 %15, %17 offset:%c27\n\t"
-                    "s_waitcnt lgkmcnt(0)"
+                    "ds_read_b64 %15, %17 offset:%c27"
                     : "=&v"(q[0][0]), "=&v"(q[0][1]), "=&v"(q[0][2]), "=&v"(q[0][3]), "=&v"(q[0][4]),
                       "=&v"(q[0][5]), "=&v"(q[0][6]), "=&v"(q[0][7]), "=&v"(q[1][0]), "=&v"(q[1][1]),
                       "=&v"(q[1][2]), "=&v"(q[1][3]), "=&v"(q[1][4]), "=&v"(q[1][5]), "=&v"(q[1][6]),
@@ -2001,6 +2000,38 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
                       "i"(8 * PW), "i"(8), "i"(16), "i"(8 * (PW + 2)), "i"(8 * (2 * PW)),
                       "i"(8 * (2 * PW + 1)), "i"(8 * (2 * PW + 2))
                     : "memory");
+            };
+            auto x_wait = [&]() {
+                asm volatile("s_waitcnt lgkmcnt(0)"
+                             : "+v"(q[0][0]), "+v"(q[0][1]), "+v"(q[0][2]), "+v"(q[0][3]), "+v"(q[0][4]),
+                               "+v"(q[0][5]), "+v"(q[0][6]), "+v"(q[0][7]), "+v"(q[1][0]), "+v"(q[1][1]),
+                               "+v"(q[1][2]), "+v"(q[1][3]), "+v"(q[1][4]), "+v"(q[1][5]), "+v"(q[1][6]),
+                               "+v"(q[1][7])
+                             :
+                             : "memory");
+            };
+            auto apply = [&](int d) {
+                if (!slow[d]) {
+                    float v = plane[addr[d]];
+                    v = v + g[d];
+                    v = v + s1[d];
+                    v = v + s3[d];
+                    v = v + s4[d];
+                    plane[addr[d]] = v;
+                } else {  // ranked rounds, as the ring kernel
+                    const int a = am[d];
+                    for (int r = 0;; ++r) {
+                        if (a >= 0 && addr[d] == r) plane[a] += g[d];
+                        asm volatile("" ::: "memory");
+                        if (__ballot(a >= 0 && addr[d] > r) == 0) break;
+                    }
+                }
+                asm volatile("" ::: "memory");
+            };
+            x_issue(0);
+            x_wait();
+#pragma unroll
+            for (int d0 = 0; d0 < D; d0 += 2) {
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     const int d = d0 + e;
@@ -2008,7 +2039,6 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
                     // q[e]: left, up, up-left, up-right, right, down-left, down, down-right
                     const bool fol = static_cast<int>(has_l & (lo(q[e][0]) == a)) | (has_u & (lo(q[e][1]) == a)) |
                                      (has_ul & (lo(q[e][2]) == a)) | (has_ur & (lo(q[e][3]) == a));
-                    // right and down-left never both match (they do not overlap)
                     const float t5 = (has_dl & (lo(q[e][5]) == a)) ? hi(q[e][5]) : -0.0f;
                     s1[d] = (has_r & (lo(q[e][4]) == a)) ? hi(q[e][4]) : t5;
                     s3[d] = (has_d & (lo(q[e][6]) == a)) ? hi(q[e][6]) : -0.0f;
@@ -2028,33 +2058,15 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
                         }
                         addr[d] = depth;
                     }
-                    const uint32_t sm8 = static_cast<uint32_t>(nx[d]) * (PHW * 8);
-                    const auto m = __builtin_amdgcn_raw_buffer_load_b64(nx[d] < 0 ? rs_m : rs_0, kl * 8, sm8, 0);
-                    cl_r[d] = m[0];
-                    ch_r[d] = m[1];
+                    mask_load(nx[d], cl_r[d], ch_r[d]);
                     fl_r[d] = nx[d] < 0;
                 }
+                if (d0 + 2 < D) x_issue(d0 + 2);
+                apply(d0);
+                apply(d0 + 1);
+                if (d0 + 2 < D) x_wait();
             }
             const unsigned long long p2 = BPROF_T();
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                if (!slow[d]) {
-                    float v = plane[addr[d]];
-                    v = v + g[d];
-                    v = v + s1[d];
-                    v = v + s3[d];
-                    v = v + s4[d];
-                    plane[addr[d]] = v;
-                } else {  // ranked rounds, as the ring kernel
-                    const int a = am[d];
-                    for (int r = 0;; ++r) {
-                        if (a >= 0 && addr[d] == r) plane[a] += g[d];
-                        asm volatile("" ::: "memory");
-                        if (__ballot(a >= 0 && addr[d] > r) == 0) break;
-                    }
-                }
-                asm volatile("" ::: "memory");
-            }
 #ifdef FRCNN_BWD_PROF
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #endif
@@ -2536,7 +2548,12 @@ BwdWs carve_bwd(void* ws, int64_t R, int N, int PH, int PW) {
 }
 constexpr size_t kPlaneBudget = 64 * 1024;       // LDS per workgroup for planes (plain kernel)
 constexpr int kBwdRing = 8;                      // RoIs in flight per wave (ring kernel)
-constexpr int kBwdLead = 6;                      // RoIs per step (leader kernel)
+// RoIs per step of the leader kernel (4: 90.5-91.5 us for the cfg5 op vs 93.1-94.1 at 6,
+// 140 at 8; -DFRCNN_BWD_LEAD_D for A/Bs)
+#ifndef FRCNN_BWD_LEAD_D
+#define FRCNN_BWD_LEAD_D 4
+#endif
+constexpr int kBwdLead = FRCNN_BWD_LEAD_D;                   // RoIs per step (leader kernel)
 constexpr size_t kPlaneBudgetRing = 144 * 1024;  // ring kernel: one workgroup per CU
 }  // namespace
 

@@ -700,7 +700,7 @@ def test_roi_pool_fwd_kernel_label():
     assert _lib.roi_pool_fwd_kernel(R, N, C, H, W, rois_sorted=False, head=False).startswith(
         "roi_pool_fwd_dense_kernel<1024, 16, 7, false, true>")
     # the backward's label follows its plan (leader kernel for 7-wide bins, ring / plain on request)
-    assert _lib.roi_pool_bwd_kernel(2048, 16, 256, 38, 38) == "roi_pool_bwd_lead_kernel<6, 7>"
+    assert _lib.roi_pool_bwd_kernel(2048, 16, 256, 38, 38) == "roi_pool_bwd_lead_kernel<4, 7>"
     assert _lib.roi_pool_bwd_kernel(2048, 16, 256, 38, 38, 5, 5) == "roi_pool_bwd_pf_kernel<8>"
     with _lib.kernel_path("roi_pool_bwd", "ring"):
         assert _lib.roi_pool_bwd_kernel(2048, 16, 256, 38, 38) == "roi_pool_bwd_pf_kernel<8>"
