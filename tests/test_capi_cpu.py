@@ -56,3 +56,28 @@ def test_argument_validation_without_gpu():
     ws = lib.frcnn_propose_workspace_size(ctypes.byref(p))
     assert ws > 2 * 6000 * 94 * 8  # holds the NMS bitmask
     assert lib.frcnn_nms_workspace_size(0) == 0
+
+
+def test_set_path_accepts_the_documented_paths_only():
+    """frcnn_set_path (host-only, no HIP call): every op / path the header documents is
+    accepted, anything else is rejected with rc=-1 and a message naming it."""
+    from replication_faster_rcnn_amd import _lib
+    lib = _lib.load(require_gpu=False)
+    ok = {"roi_pool_fwd": ["auto", "wave", "pair", "key", "dense", "generic"],
+          "roi_pool_bwd": ["auto", "ring", "plain"],
+          "propose": ["auto", "hybrid", "lazy", "wide"],
+          "roi_pool_fwd_store": ["auto", "temporal", "nt"],
+          "sampler": ["auto", "walk", "chip"],
+          "roi_pool_split": ["auto", "0", "7", "64"],
+          "roi_pool_cg": ["auto", "4", "8", "16"]}
+    try:
+        for op, paths in ok.items():
+            for p in paths:
+                assert lib.frcnn_set_path(op.encode(), p.encode()) == 0, (op, p)
+        for op, p in [("roi_pool_fwd_store", "streaming"), ("roi_pool_split", "65"), ("roi_pool_split", "x"),
+                      ("roi_pool_cg", "2"), ("sampler", "tiles"), ("no_such_op", "auto")]:
+            assert lib.frcnn_set_path(op.encode(), p.encode()) == -1, (op, p)
+            assert p.encode() in lib.frcnn_last_error()
+    finally:
+        for op in ok:
+            lib.frcnn_set_path(op.encode(), b"auto")
