@@ -10,9 +10,11 @@ input already resident in HBM:
     -> RoI transform + pack + RoIPool forward (nets/heads.py:42-48, one launch)
 
 Configs (BASELINE.json): --config auto = cfg2 (configs[1]: 8 images of
-600x1000, 6000->300, RoIPool 7x7x256) on one GPU, cfg3 (configs[2]: 64 images
-sharded per image over the N GPUs, strong scaling) for N > 1.  cfg1 / cfg4 are
-the single-image configs, cfg5 the training step (configs[4]).
+600x1000, 6000->300, RoIPool 7x7x256) per GPU at every N ("scaling": "weak";
+the global batch is 8N images sharded per image, so N = 8 is configs[2]'s
+64-image batch over 8 GPUs).  --config cfg3 runs those 64 images strong-scaled
+over the N GPUs; cfg1 / cfg4 are the single-image configs, cfg5 the training
+step (configs[4]).
 
 Multi-GPU: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set)
 each process is one rank; `python bench.py --gpus N` without it starts
@@ -67,7 +69,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="auto",
-                    help="auto (cfg2 at N=1, cfg3 at N>1) | cfg1 | cfg2 | cfg3 | cfg4 | cfg5")
+                    help="auto (cfg2 per GPU at every N, weak scaling) | cfg1 | cfg2 | cfg3 | cfg4 | cfg5")
     ap.add_argument("--streams", type=int, default=2, choices=(1, 2),
                     help="2: the proposal layer of step k+1 runs on its own HIP stream beside "
                          "step k's RoIPool (each step still does all of its work)")
@@ -171,9 +173,27 @@ def setup_dist(args):
 
 
 def resolve_config(args, world):
+    """--config auto = cfg2 (configs[1]: 8 images per GPU) at EVERY N: the 1/2/4/8-GPU
+    curve is one workload weak-scaled, 8 images per rank, so N = 8 runs the 64-image
+    global batch of configs[2] (cfg3) sharded per image and N = 1 is the headline
+    line.  --config cfg3 keeps the strong-scaled 64-image batch."""
     if args.config != "auto":
         return args.config
-    return "cfg2" if world == 1 else "cfg3"
+    return "cfg2"
+
+
+def workload_name(cfg, c, N, n_total, world, C, train):
+    """The record's config.workload: names the per-GPU workload the same way at every N."""
+    K = 3 * len(c["scales"])
+    if train:
+        return (f"{cfg}: training step, {N} images/GPU {c['img_h']}x{c['img_w']}, "
+                f"{c['feat_h']}x{c['feat_w']}x{K} anchors, {c['pre_nms']}->{c['post_nms']} NMS@0.7, "
+                f"anchor targets vs 32 gt + proposal targets (128/img), RoIPool 7x7x{C} fwd+bwd")
+    shard_txt = (f"{n_total} images sharded per image over {world} ranks" if cfg == "cfg3"
+                 else f"{c['batch']} images/GPU")
+    return (f"{cfg}: {shard_txt}, VOC shape {c['img_h']}x{c['img_w']}, "
+            f"{c['feat_h']}x{c['feat_w']}x{K} anchors, {c['pre_nms']}->{c['post_nms']} NMS@0.7, "
+            f"RoIPool 7x7x{C}")
 
 
 def make_inputs(cfg, images, device, seed=0):
@@ -763,28 +783,19 @@ def main():
         # creators' draws walk numpy's sequential MT19937 stream, one workgroup
         # each (at_sample_kernel, then pt_sample_kernel) on the draws' stream
         dr = ev["draw"]  # the draws' stream period: one record per step after the second sampler
-        draw_us = float(np.mean([a.elapsed_time(b) for a, b in zip(dr[:-1], dr[1:])])) * 1e3
+        gaps = [a.elapsed_time(b) for a, b in zip(dr[:-1], dr[1:])]
+        draw_us = float(np.mean(gaps)) * 1e3 if gaps else None  # (--steps 1: no period)
         pool_roof["fwd_event_interval_us_in_pipeline"] = fwd_ms * 1e3
         roof = {"bound": "latency", "kernel": "at_sample_kernel", "unit": "us/step",
                 "achieved": draw_us, "peak": None, "frac": None, "traffic": None,
                 "basis": "the draws' stream period (at_sample_kernel + pt_sample_kernel, one 1024-thread "
                          "workgroup each, sequential MT19937 stream, + the stream's wait / record packets) "
                          "between consecutive steps, HIP events; latency-bound, so no HBM / MFMA peak applies",
-                "draws_share_of_step": draw_us / (ms_step * 1e3),
+                "draws_share_of_step": None if draw_us is None else draw_us / (ms_step * 1e3),
                 "roi_pool_bwd": pool_roof}
         pool_roof = roof
     images = n_total * args.steps
-    K = 3 * len(c["scales"])
-    if train:
-        workload = (f"{cfg}: training step, {N} images/GPU {c['img_h']}x{c['img_w']}, "
-                    f"{c['feat_h']}x{c['feat_w']}x{K} anchors, {c['pre_nms']}->{c['post_nms']} NMS@0.7, "
-                    f"anchor targets vs 32 gt + proposal targets (128/img), RoIPool 7x7x{C} fwd+bwd")
-    else:
-        shard_txt = (f"{n_total} images sharded per image over {world} ranks ({N} on rank 0)"
-                     if cfg == "cfg3" else f"{N} images/GPU")
-        workload = (f"{cfg}: {shard_txt}, VOC shape {c['img_h']}x{c['img_w']}, "
-                    f"{c['feat_h']}x{c['feat_w']}x{K} anchors, {c['pre_nms']}->{c['post_nms']} NMS@0.7, "
-                    f"RoIPool 7x7x{C}")
+    workload = workload_name(cfg, c, N, n_total, world, C, train)
     rec = {
         "metric": "images/sec through RPN proposal+NMS+RoIPool; RoIPool HBM GB/s vs peak",
         "value": images / el, "unit": "images/sec", "n_gpus": world, "steps": args.steps,
@@ -793,7 +804,7 @@ def main():
         "data": f"synthetic, {len(sets)} input sets of {set_bytes / 2**20:.1f} MiB cycled (HBM-resident, "
                 f"{len(sets) * set_bytes / 2**20:.0f} MiB > the 256 MiB Infinity Cache)"
                 if len(sets) * set_bytes > (256 << 20) else f"synthetic, {len(sets)} input set(s) cycled",
-        "config": {"workload": workload, "global_batch": n_total,
+        "config": {"workload": workload, "global_batch": n_total, "images_per_gpu": N,
                    "parallelism": f"dp{world} (per-image sharding)", "streams": args.streams,
                    "prop_streams": args.prop_streams if (args.streams == 2 and not train) else 1,
                    "pool_on": args.pool_on if (args.streams == 2 and not train) else None,
