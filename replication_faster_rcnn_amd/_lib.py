@@ -86,7 +86,6 @@ SIGNATURES = {
 DEBUG_SIGNATURES = {
     "frcnn_debug_sampler_prof": (I32, [P, I32]),  # -DFRCNN_SAMPLER_PROF (tools/probe_sampler.py)
     "frcnn_debug_key_prof": (I32, [P, I32]),      # -DFRCNN_KEY_PROF (tools/dbg/key_prof.py)
-    "frcnn_debug_sort_prof": (I32, [P, I32]),     # -DFRCNN_SORT_PROF (tools/dbg/sort_prof.py)
     "frcnn_debug_draw_hdr": (I32, [I32, I32, I32, I32, I32, P, P]),  # tools/probe_draws.py
 }
 

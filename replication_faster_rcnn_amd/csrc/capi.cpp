@@ -68,9 +68,8 @@ extern "C" int frcnn_set_path(const char* op, const char* path) {
     const bool aut = is(path, "auto");
     if (is(op, "roi_pool_fwd") &&
         (aut || is(path, "pair") || is(path, "wave") || is(path, "key") || is(path, "dense") ||
-         is(path, "generic") || is(path, "sort"))) {
+         is(path, "generic"))) {
         g_path.roi_fwd = aut ? kPathAuto : is(path, "generic") ? kPathGeneric
-                                       : is(path, "sort")      ? kPathSort
                                        : is(path, "dense")     ? kPathDense
                                        : is(path, "pair")      ? kPathPair
                                        : is(path, "key")       ? kPathKey

@@ -21,7 +21,6 @@ constexpr int kPathDense = 2;    // roi_pool_fwd: image tile, RoI bins packed pe
 constexpr int kPathWave = 3;     // roi_pool_fwd: image tile, one wave per RoI (RoIs grouped by image)
 constexpr int kPathPair = 4;     // roi_pool_fwd: raw + pixel-pair tiles, one wave per RoI (grouped by image)
 constexpr int kPathKey = 5;      // roi_pool_fwd: ordered-key tile, two-maximum scan, one wave per RoI (grouped by image)
-constexpr int kPathSort = 6;     // roi_pool_fwd: image tile, bins sorted by window shape, 64 per round (grouped by image)
 constexpr int kPathPlain = 1;    // roi_pool_bwd: the unpipelined plane-owner kernel
 constexpr int kPathRing = 2;     // roi_pool_bwd: the RoI-at-a-time ring kernel (auto: leader kernel)
 constexpr int kPathHybrid = 1;   // propose: fused per image + chip-wide first-chunk mask

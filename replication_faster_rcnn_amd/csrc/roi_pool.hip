@@ -1358,523 +1358,6 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_key_kernel(
     PPROF_T(3);
 }
 
-// ------------------------------------------------- row-sorted forward
-// One 1024-thread workgroup owns 8 channel planes of one image (tile: pixel p
-// at LDS bytes [32p, 32p + 32), its 8 channels) and a strided share of that
-// image's RoIs (items z, z+split, ..., like the wave kernel).  Work is cut by
-// window ROW instead of by RoI:
-//   * the share's RoIs are ordered by window class (largest bin height,
-//     width) and cut into chunks of K RoIs (K*PH <= 64 rows: K = 9 at 7x7);
-//     each chunk's rows (k, ph) are ordered by bin height, descending (one
-//     wave per chunk, a ballot counting sort, before the RoIs are pooled);
-//   * a round = 64 / PW consecutive rows of that order (9 at 7x7), a lane =
-//     one bin x 8 channels: the wave walks the round's largest window (maxh x
-//     maxw) and every lane clamps its row / column to its own window (a re-read
-//     pixel never passes the strict '>' again, so the result is torchvision's).
-//     Rows of one round share their height, so the lanes do nearly the same
-//     work: at cfg2 0.78 of the update slots are useful against 0.52 for the
-//     wave-per-RoI kernel, which walks each RoI's largest window on 49 lanes;
-//   * the index update takes the step's offset dh*W + dw from a scalar, the
-//     lane's window origin is added once at the end;
-//   * results go to an LDS staging block per RoI ([c][bin] fp32 values and
-//     u16 argmax + 1) and leave as whole 16-B stores per lane (1,568
-//     contiguous bytes per RoI and output at 7x7).
-// Tasks: every wave claims the next task of one stream from an LDS counter:
-// step t = [flush tasks of chunk t-3] [rounds of chunk t], chunk j staged in
-// slot j % 3.  A round of chunk j waits (a counter in LDS) until the flush
-// of chunk j-3 has read slot j % 3; a flush task of chunk j waits until every
-// round of chunk j is in.  Waits point only at earlier tasks, which never
-// wait on later ones, so the stream cannot deadlock; the counters only grow
-// within a segment (no resets to race with).
-// LDS (dynamic): tile HW*32 | 3 slots x K*PHW*48 | geometry cap x int4 |
-//   RoI index cap x int | row lists cap*PH u8.  Before the ring runs, the
-//   first slot holds the RoI class histogram.
-#ifndef FRCNN_SORT_X
-#define FRCNN_SORT_X 0  // experiment builds only: 1 no scan, 2 no staging writes, 4 no flush stores, 8 no waits
-#endif
-#ifdef FRCNN_SORT_PROF  // timeline probe (experiment builds): per workgroup 100-MHz stamps
-__device__ unsigned long long g_sort_prof[4096][6];
-#define SPROF(k)                                                                                  \
-    do {                                                                                          \
-        const unsigned _wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);     \
-        if (_wg < 4096 && threadIdx.x == 0) g_sort_prof[_wg][k] = __builtin_amdgcn_s_memrealtime(); \
-    } while (0)
-#define SPROF_MAX(k)                                                                              \
-    do {                                                                                          \
-        const unsigned _wg = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);     \
-        if (_wg < 4096 && (threadIdx.x & 63) == 0) atomicMax(&g_sort_prof[_wg][k], __builtin_amdgcn_s_memrealtime()); \
-    } while (0)
-#else
-#define SPROF(k) do {} while (0)
-#define SPROF_MAX(k) do {} while (0)
-#endif
-constexpr int kSortCG = 8;
-constexpr int kSortMaxSlots = 16;
-constexpr int kSortFlushRois = 3;  // RoIs per flush task
-// a staging slot: one u16 code per output (8 channels x PHW bins x K RoIs)
-__host__ __device__ constexpr size_t sort_slot_bytes(int KP) { return (static_cast<size_t>(KP) * 16 + 15) & ~static_cast<size_t>(15); }
-__host__ __device__ constexpr size_t sort_a16(size_t b) { return (b + 15) & ~static_cast<size_t>(15); }
-// per RoI: geometry int4, RoI index int, row list PH u8, row windows PH u16, column windows PW u16;
-// per chunk of K RoIs: round maxima 16 u16 (K >= 4, rounds <= 16: chunks <= cap / 4 + 1)
-__host__ __device__ constexpr size_t sort_roi_bytes(int cap, int PH, int PW) {
-    return static_cast<size_t>(cap) * (16 + 4) + sort_a16(static_cast<size_t>(cap) * PH) +
-           sort_a16(static_cast<size_t>(cap) * PH * 2) + sort_a16(static_cast<size_t>(cap) * PW * 2) +
-           sort_a16(static_cast<size_t>(cap) * 8 + 64);
-}
-__host__ __device__ constexpr size_t sort_lds_bytes(int HW, int K, int PH, int PW, int cap, int slots) {
-    return static_cast<size_t>(HW + 1) * 32 + slots * sort_slot_bytes(K * PH * PW) + sort_roi_bytes(cap, PH, PW);
-}
-
-// Rows [hs, he) of bin row ph and columns [ws, we) of bin column pw
-// (torchvision's bin boundaries, as geom_bin).
-__device__ __forceinline__ int2 geom_rows(const RoiGeom& g, int H, int ph) {
-    const int hs = static_cast<int>(floorf(static_cast<float>(ph) * g.bh)) + g.sh;
-    const int he = static_cast<int>(ceilf(static_cast<float>(ph + 1) * g.bh)) + g.sh;
-    return make_int2(min(max(hs, 0), H), min(max(he, 0), H));
-}
-__device__ __forceinline__ int2 geom_cols(const RoiGeom& g, int W, int pw) {
-    const int ws = static_cast<int>(floorf(static_cast<float>(pw) * g.bw)) + g.sw;
-    const int we = static_cast<int>(ceilf(static_cast<float>(pw + 1) * g.bw)) + g.sw;
-    return make_int2(min(max(ws, 0), W), min(max(we, 0), W));
-}
-__device__ __forceinline__ RoiGeom geom_of_int4(int4 q) {
-    RoiGeom g;
-    g.sh = q.x;
-    g.sw = q.y;
-    g.bh = __int_as_float(q.z);
-    g.bw = __int_as_float(q.w);
-    return g;
-}
-// Wave-wide maxima of two small non-negative ints (< 65536), packed.
-__device__ __forceinline__ int2 wave_max2(int a, int b) {
-    uint32_t p = (static_cast<uint32_t>(a) << 16) | static_cast<uint32_t>(b);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t q = static_cast<uint32_t>(__shfl_xor(static_cast<int>(p), o, 64));
-        p = (max(p >> 16, q >> 16) << 16) | max(p & 0xFFFFu, q & 0xFFFFu);
-    }
-    return make_int2(__builtin_amdgcn_readfirstlane(static_cast<int>(p >> 16)),
-                     __builtin_amdgcn_readfirstlane(static_cast<int>(p & 0xFFFFu)));
-}
-__device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-// A ring counter bumped by one wave: every lane adds 1 (the counter counts
-// 64 per wave), so the add stays in the wave's uniform control flow and the
-// atomic optimizer makes it ONE LDS atomic of popcount(exec).  (A lane-
-// predicated LDS store here was sunk by the structurizer into a later block
-// with another iteration's operands; a per-lane value (lane == 0 ? 1 : 0)
-// makes the optimizer sum the lanes in a 64-trip SALU loop, and the CU's 16
-// waves then queue on its scalar unit: 67 us of a 77-us skeleton, round 5.)
-constexpr int kRingInc = 64;
-__device__ __forceinline__ void ring_bump(int* ctr) {
-    lds_order();
-    __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// Wait until *ctr >= want (bounded: a ring bug shows as wrong outputs, never as a hung GPU).
-__device__ __forceinline__ void ring_wait(int* ctr, int want) {
-    if (FRCNN_SORT_X & 8) return;
-    for (int spin = 0; spin < (1 << 22); ++spin) {
-        const int v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (v >= want) break;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    lds_order();
-}
-
-// One pixel step of a round: the 8 channels against the running (max, step)
-// pairs -- torchvision's strict '>' moves the index; the running maximum is a
-// v_max_f32 (no NaN in the tile: staged as -inf; the sign of a zero maximum is
-// re-read after the walk), which sits between the compare and the index
-// select and so fills the compare's VCC hazard slot.
-__device__ __forceinline__ float vmax_raw(float a, float b) {
-    float d;
-    asm("v_max_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
-    return d;
-}
-// Two channels per asm block, each compare two instructions ahead of its select
-// (gfx950 wants 2 wait states between a VALU mask write and v_cndmask): no s_nop.
-__device__ __forceinline__ void upd2(float a0, float a1, float& m0, float& m1, int& i0, int& i1, int st) {
-    uint64_t t;
-    asm volatile(
-        "v_cmp_gt_f32 vcc, %5, %0\n\t"
-        "v_max_f32 %0, %0, %5\n\t"
-        "v_cmp_gt_f32 %4, %6, %1\n\t"
-        "v_cndmask_b32 %2, %2, %7, vcc\n\t"
-        "v_max_f32 %1, %1, %6\n\t"
-        "v_cndmask_b32 %3, %3, %7, %4"
-        : "+v"(m0), "+v"(m1), "+v"(i0), "+v"(i1), "=&s"(t)
-        : "v"(a0), "v"(a1), "v"(st)
-        : "vcc");
-}
-__device__ __forceinline__ void sort_update(const float4 v0, const float4 v1, float (&mv)[8], int (&mi)[8],
-                                            int step) {
-    upd2(v0.x, v0.y, mv[0], mv[1], mi[0], mi[1], step);
-    upd2(v0.z, v0.w, mv[2], mv[3], mi[2], mi[3], step);
-    upd2(v1.x, v1.y, mv[4], mv[5], mi[4], mi[5], step);
-    upd2(v1.z, v1.w, mv[6], mv[7], mi[6], mi[7], step);
-}
-
-// The round's walk for maxw == MW (a compile-time width): per row, groups of
-// <= 4 pixel reads issued together, then the updates; lanes with a narrower or
-// shorter window re-read their last column / row.
-template <int MW>
-__device__ __forceinline__ void sort_scan(const char* __restrict__ tile, uint32_t base, int W, int maxh, int hl,
-                                          int wl, float (&mv)[8], int (&mi)[8]) {
-    uint32_t coff[MW];
-#pragma unroll
-    for (int dw = 0; dw < MW; ++dw) coff[dw] = static_cast<uint32_t>(min(dw, wl)) * 32u;
-    const uint32_t rs = static_cast<uint32_t>(W) * 32u;
-    for (int dh = 0; dh < maxh; ++dh) {
-        const uint32_t ra = base + static_cast<uint32_t>(min(dh, hl)) * rs;
-        const int srow = dh * W;
-#pragma unroll
-        for (int g0 = 0; g0 < MW; g0 += 4) {
-            constexpr int G = MW < 4 ? MW : 4;
-            float4 v[G][2];
-#pragma unroll
-            for (int i = 0; i < G; ++i) {
-                if (g0 + i < MW) {
-                    const float4* pp = reinterpret_cast<const float4*>(tile + ra + coff[g0 + i]);
-                    v[i][0] = pp[0];
-                    v[i][1] = pp[1];
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int i = 0; i < G; ++i)
-                if (g0 + i < MW) sort_update(v[i][0], v[i][1], mv, mi, srow + g0 + i);
-        }
-    }
-}
-// Any width: one pixel at a time, the column clamp per step.
-__device__ __forceinline__ void sort_scan_any(const char* __restrict__ tile, uint32_t base, int W, int maxh,
-                                              int maxw, int hl, int wl, float (&mv)[8], int (&mi)[8]) {
-    const uint32_t rs = static_cast<uint32_t>(W) * 32u;
-    for (int dh = 0; dh < maxh; ++dh) {
-        const uint32_t ra = base + static_cast<uint32_t>(min(dh, hl)) * rs;
-        const int srow = dh * W;
-        for (int dw = 0; dw < maxw; ++dw) {
-            const float4* pp = reinterpret_cast<const float4*>(tile + ra + static_cast<uint32_t>(min(dw, wl)) * 32u);
-            sort_update(pp[0], pp[1], mv, mi, srow + dw);
-        }
-    }
-}
-
-template <int NT, int FIX, bool HEAD>
-__global__ __launch_bounds__(NT) void roi_pool_fwd_sort_kernel(
-    const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W, int PH_, int PW_,
-    float ss, float* __restrict__ out, int32_t* __restrict__ argmax, int K, int cap, int NS, HeadArgs hd) {
-    constexpr int CG = kSortCG;
-    const int PH = FIX ? FIX : PH_, PW = FIX ? FIX : PW_;
-    const int PHW = PH * PW;
-    extern __shared__ __attribute__((aligned(16))) float4 smem4[];
-    __shared__ int s_red[2 * (NT / 64)];
-    __shared__ int s_ctl[1 + 2 * kSortMaxSlots];  // 0 next task; 1.. rounds done per slot; 1+S.. flush tasks done per slot
-    const int b = blockIdx.z;
-    const int c0 = blockIdx.x * CG;
-    const int tid = threadIdx.x, lane = tid & 63;
-    // wave-uniform values go through readfirstlane so the compiler keeps them in
-    // SGPRs and every branch of the ring below scalar
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int HW = H * W;
-    const int split = gridDim.y, z = blockIdx.y;
-    const int N = gridDim.z - 1;
-    if (b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
-        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, 0, N, s_red, 1)
-                             : roi_range_sorted<NT>(rois, R, 0, N, s_red);
-        const int n_lo = rg.x, tot = n_lo + (R - rg.y);
-        const int lo = static_cast<int>(static_cast<int64_t>(tot) * z / split);
-        const int hi = static_cast<int>(static_cast<int64_t>(tot) * (z + 1) / split);
-        if (HEAD && hd.boxes && blockIdx.x == 0)
-            for (int t = lo + tid; t < hi; t += NT) {
-                const int r = t < n_lo ? t : rg.y + (t - n_lo);
-                float bx[5];
-                head_box(rois, hd, r, bx);
-#pragma unroll
-                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
-            }
-        for (int e = lo * CG * PHW + tid; e < hi * CG * PHW; e += NT) {
-            const int t = e / (CG * PHW);
-            const int rem = e - t * (CG * PHW);
-            const int r = t < n_lo ? t : rg.y + (t - n_lo);
-            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + rem;
-            out[o] = 0.0f;
-            argmax[o] = -1;
-        }
-        return;
-    }
-    const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, b, b + 1, s_red, 1)
-                         : roi_range_sorted<NT>(rois, R, b, b + 1, s_red);
-    const int rbase = __builtin_amdgcn_readfirstlane(rg.x);
-    const int nr = __builtin_amdgcn_readfirstlane(rg.y) - rbase;
-    if (z >= nr) return;
-    const int nmine = (nr - z + split - 1) / split;  // items z, z+split, ...
-    SPROF(0);
-
-    // ---- LDS carve (sort_lds_bytes)
-    const int KP = K * PHW;
-    const size_t slot_b = sort_slot_bytes(KP);
-    char* tile = reinterpret_cast<char*>(smem4);
-    char* slots = tile + static_cast<size_t>(HW + 1) * 32;
-    int4* t_geo = reinterpret_cast<int4*>(slots + NS * slot_b);
-    int* t_rid = reinterpret_cast<int*>(t_geo + cap);
-    uint8_t* t_rows = reinterpret_cast<uint8_t*>(t_rid + cap);                              // [cap*PH] k << 4 | ph
-    uint16_t* t_rw = reinterpret_cast<uint16_t*>(t_rows + sort_a16(static_cast<size_t>(cap) * PH));  // hs | he << 8
-    uint16_t* t_cw = t_rw + sort_a16(static_cast<size_t>(cap) * PH * 2) / 2;                 // ws | we << 8
-    uint16_t* t_rmax = t_cw + sort_a16(static_cast<size_t>(cap) * PW * 2) / 2;               // maxh | maxw << 8
-    unsigned* hist = reinterpret_cast<unsigned*>(slots);  // RoI class histogram (before the ring)
-
-    // ---- stage the 8 channel planes: pixel p -> tile[32p, 32p + 32); NaN -> -inf (never
-    // selected by the strict '>' either way); pixel HW = the all -inf sentinel empty bins walk
-    {
-        const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
-        for (int p = tid; p <= HW; p += NT) {
-            float v[CG];
-#pragma unroll
-            for (int q = 0; q < CG; ++q) {
-                const float e = p < HW ? src[static_cast<size_t>(q) * HW + p] : -INFINITY;
-                v[q] = e != e ? -INFINITY : e;
-            }
-            float4* d = reinterpret_cast<float4*>(tile + static_cast<size_t>(p) * 32);
-            d[0] = make_float4(v[0], v[1], v[2], v[3]);
-            d[1] = make_float4(v[4], v[5], v[6], v[7]);
-        }
-    }
-    const int RPR = 64 / PW;  // rows per round
-    const int rfull = (K * PH + RPR - 1) / RPR;
-    const int ffull = (K + kSortFlushRois - 1) / kSortFlushRois;
-    const int SS = ffull + rfull;  // tasks per step
-
-    for (int s0 = 0; s0 < nmine; s0 += cap) {
-        const int ns = min(cap, nmine - s0);
-        // ---- (a) RoI table: geometry, bin windows, window class; counting-sorted by class (descending)
-        for (int i = tid; i < 256; i += NT) hist[i] = 0;
-        if (tid < 1 + 2 * kSortMaxSlots) s_ctl[tid] = 0;
-        __syncthreads();  // tile staged; the previous segment is done with the table and the slots
-        SPROF(1);
-        int4 mygeo = make_int4(0, 0, 0, 0);
-        int myr = 0, mykey = 0;
-        uint32_t rwin[8], cwin[8];  // this RoI's row / column windows, two u16 (lo | hi << 8) per word
-        if (tid < ns) {
-            myr = rbase + z + (s0 + tid) * split;
-            float bx[5];
-            if (HEAD) {
-                head_box(rois, hd, myr, bx);
-                if (hd.boxes && blockIdx.x == 0) {
-#pragma unroll
-                    for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(myr) * 5 + j] = bx[j];
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 5; ++j) bx[j] = rois[static_cast<size_t>(myr) * 5 + j];
-            }
-            const RoiGeom gm = roi_geom(bx, ss, PH, PW);
-            mygeo = make_int4(gm.sh, gm.sw, __float_as_int(gm.bh), __float_as_int(gm.bw));
-            int mh = 0, mw = 0;
-#pragma unroll
-            for (int p = 0; p < 16; ++p) {
-                if (p < PH) {
-                    const int2 hr = geom_rows(gm, H, p);
-                    mh = max(mh, hr.y - hr.x);
-                    const uint32_t w16 = static_cast<uint32_t>(hr.x | (hr.y << 8));
-                    if (p & 1) rwin[p >> 1] |= w16 << 16; else rwin[p >> 1] = w16;
-                }
-                if (p < PW) {
-                    const int2 wr = geom_cols(gm, W, p);
-                    mw = max(mw, wr.y - wr.x);
-                    const uint32_t w16 = static_cast<uint32_t>(wr.x | (wr.y << 8));
-                    if (p & 1) cwin[p >> 1] |= w16 << 16; else cwin[p >> 1] = w16;
-                }
-            }
-            mykey = (mh > 0 && mw > 0) ? (min(mh, 15) << 4) | min(mw, 15) : 0;
-            atomicAdd(&hist[255 - mykey], 1u);
-        }
-        __syncthreads();
-        if (wid == 0) {  // exclusive scan of the 256 buckets, 4 per lane
-            unsigned h[4], loc = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                h[j] = hist[4 * lane + j];
-                loc += h[j];
-            }
-            unsigned incl = loc;
-            for (int o = 1; o < 64; o <<= 1) {
-                const unsigned v = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += v;
-            }
-            unsigned run = incl - loc;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                hist[4 * lane + j] = run;
-                run += h[j];
-            }
-        }
-        __syncthreads();
-        if (tid < ns) {
-            const unsigned pos = atomicAdd(&hist[255 - mykey], 1u);
-            t_geo[pos] = mygeo;
-            t_rid[pos] = myr;
-#pragma unroll
-            for (int p = 0; p < 16; ++p) {
-                if (p < PH) t_rw[pos * PH + p] = static_cast<uint16_t>(rwin[p >> 1] >> (16 * (p & 1)));
-                if (p < PW) t_cw[pos * PW + p] = static_cast<uint16_t>(cwin[p >> 1] >> (16 * (p & 1)));
-            }
-        }
-        __syncthreads();
-        const int nch = (ns + K - 1) / K;
-        const int klast = ns - (nch - 1) * K;
-        // ---- (b) each chunk's rows ordered by bin height (descending) and each round's
-        // window bound (maxh, maxw): one wave per chunk, a lane per row (K * PH <= 64),
-        // a ballot counting sort; the sorted rows' (height, widest column of the RoI)
-        // pass through a per-wave scratch row at the start of the slots (the class
-        // histogram is done; the ring has not started; sort_plan keeps 3 slots >= 2 KiB)
-        uint16_t* scr = reinterpret_cast<uint16_t*>(slots) + wid * 64;
-        for (int j = wid; j < nch; j += NT / 64) {
-            const int nk = j == nch - 1 ? klast : K;
-            const bool live = lane < nk * PH;
-            const int k = live ? lane / PH : 0, ph = live ? lane - (lane / PH) * PH : 0;
-            const int rw = t_rw[(j * K + k) * PH + ph];
-            int mwk = 0;  // the RoI's widest column
-            for (int p = 0; p < PW; ++p) {
-                const int cw = t_cw[(j * K + k) * PW + p];
-                mwk = max(mwk, (cw >> 8) - (cw & 0xFF));
-            }
-            const int hgt = (rw >> 8) - (rw & 0xFF);
-            const int key = live ? (mwk > 0 ? min(hgt, 15) : 0) : -1;
-            int base = 0, pos = 0;
-            for (int h = 15; h >= 0; --h) {
-                const uint64_t m = __ballot(key == h);
-                if (key == h) pos = base + static_cast<int>(__popcll(m & lanemask_lt()));
-                base += static_cast<int>(__popcll(m));
-            }
-            const int rh = (mwk > 0) ? min(hgt, 255) : 0, rwid = (hgt > 0) ? min(mwk, 255) : 0;
-            if (live) {
-                t_rows[j * K * PH + pos] = static_cast<uint8_t>((k << 4) | ph);
-                scr[pos] = static_cast<uint16_t>(rh | (rwid << 8));
-            }
-            lds_order();
-            const int nrnd = (nk * PH + RPR - 1) / RPR;
-            if (lane < nrnd) {  // lane r: round r's bound over its rows
-                int mh = 0, mw = 0;
-                for (int i = lane * RPR; i < min((lane + 1) * RPR, nk * PH); ++i) {
-                    const int v = scr[i];
-                    mh = max(mh, v & 0xFF);
-                    mw = max(mw, v >> 8);
-                }
-                t_rmax[j * 16 + lane] = static_cast<uint16_t>(mh | (mw << 8));
-            }
-            lds_order();  // (the wave's next chunk rewrites its scratch row)
-        }
-        __syncthreads();  // the row lists are in; the class histogram is done with slot 0
-        SPROF(2);
-
-        // ---- (c) the task stream: step t = [ffull flush tasks of chunk t-3] [rfull rounds of
-        // chunk t] (tasks past a chunk's RoIs / rounds are empty)
-        const int total = (nch + NS) * SS;
-        while (true) {
-            int g = 0;
-            if (lane == 0) g = atomicAdd(&s_ctl[0], 1);
-            g = __builtin_amdgcn_readfirstlane(g);
-            if (g >= total) break;
-            const int step = g / SS, off = g - step * SS;
-            if (off < ffull) {
-                // ---- flush task: RoIs [off*FR, ...) of chunk jf, once all its rounds are in
-                const int jf = step - NS;
-                if (jf < 0) continue;
-                const int sl = jf % NS, m = jf / NS;
-                const int nk = jf == nch - 1 ? klast : K;
-                const int k0 = off * kSortFlushRois, k1 = min(k0 + kSortFlushRois, nk);
-                if (k0 >= k1) continue;
-                const int nrj = jf == nch - 1 ? (klast * PH + RPR - 1) / RPR : rfull;
-                ring_wait(&s_ctl[1 + sl], kRingInc * (rfull * m + nrj));
-                // a code per output: 0xFFFF empty bin (0, -1); 0 nothing passed (-FLT_MAX, -1);
-                // else argmax + 1, the value re-read from the tile (exact bits, zero signs too)
-                const char* sb = slots + slot_b * sl;
-                const int per = 2 * PHW;  // float4 per RoI block (8 channels x PHW)
-                const float* tf = reinterpret_cast<const float*>(tile);
-                for (int k = k0; k < k1; ++k) {  // one RoI's block at a time: scalar bases
-                    const int r = __builtin_amdgcn_readfirstlane(t_rid[jf * K + k]);
-                    float4* ov = reinterpret_cast<float4*>(out) + (static_cast<size_t>(r) * C + c0) * PHW / 4;
-                    int4* oi = reinterpret_cast<int4*>(argmax) + (static_cast<size_t>(r) * C + c0) * PHW / 4;
-                    const uint2* lc = reinterpret_cast<const uint2*>(sb) + k * per;
-                    for (int f = lane; f < per; f += 64) {
-                        const uint2 cv = lc[f];
-                        const uint32_t code[4] = {cv.x & 0xFFFFu, cv.x >> 16, cv.y & 0xFFFFu, cv.y >> 16};
-                        float v[4];
-                        int ix[4];
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const int c = (4 * f + i) / PHW;
-                            const int q = static_cast<int>(code[i]) - 1;
-                            const bool hit = code[i] != 0u && code[i] != 0xFFFFu;
-                            v[i] = hit ? tf[q * 8 + c] : (code[i] == 0u ? -FLT_MAX : 0.0f);
-                            ix[i] = hit ? q : -1;
-                        }
-                        if (!(FRCNN_SORT_X & 4)) {
-                            ov[f] = make_float4(v[0], v[1], v[2], v[3]);
-                            oi[f] = make_int4(ix[0], ix[1], ix[2], ix[3]);
-                        }
-                    }
-                }
-                ring_bump(&s_ctl[1 + kSortMaxSlots + sl]);  // (the staging reads are complete)
-                continue;
-            }
-            // ---- round t of chunk j: RPR rows of the height-sorted list
-            const int j = step, t = off - ffull;
-            if (j >= nch) continue;
-            const int nk = j == nch - 1 ? klast : K;
-            if (t * RPR >= nk * PH) continue;
-            const int sl = j % NS, m = j / NS;
-            if (m > 0) ring_wait(&s_ctl[1 + kSortMaxSlots + sl], kRingInc * ffull * m);  // chunk j-NS flushed
-            const int rs = lane / PW, pw = lane - rs * PW;
-            const int ri = t * RPR + rs;
-            const bool valid = rs < RPR && ri < nk * PH;
-            const int ent = valid ? t_rows[j * K * PH + ri] : 0;
-            const int k = ent >> 4, ph = ent & 15;
-            const int rwv = t_rw[(j * K + k) * PH + ph], cwv = t_cw[(j * K + k) * PW + pw];
-            const int rmx = __builtin_amdgcn_readfirstlane(static_cast<int>(t_rmax[j * 16 + t]));
-            const int maxh = rmx & 0xFF, maxw = rmx >> 8;
-            const int hs = rwv & 0xFF, ws = cwv & 0xFF;
-            const int hh = (rwv >> 8) - hs, ww = (cwv >> 8) - ws;
-            const bool empty = !valid || hh <= 0 || ww <= 0;
-            // empty bins walk the -inf sentinel from (0, -1); the others start at (-FLT_MAX,
-            // -(p0 + 1)), so argmax + 1 = mi + p0 + 1 is 0 until a pixel passes
-            const int p0 = empty ? 0 : hs * W + ws;
-            float mv[8];
-            int mi[8];
-#pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                mv[c] = empty ? 0.0f : -FLT_MAX;
-                mi[c] = -(p0 + 1);
-            }
-            if (maxh > 0 && !(FRCNN_SORT_X & 1)) {
-                const uint32_t base = static_cast<uint32_t>(empty ? HW : p0) * 32u;
-                const int hl = empty ? 0 : hh - 1, wl = empty ? 0 : ww - 1;
-                switch (maxw) {
-                    case 1: sort_scan<1>(tile, base, W, maxh, hl, wl, mv, mi); break;
-                    case 2: sort_scan<2>(tile, base, W, maxh, hl, wl, mv, mi); break;
-                    case 3: sort_scan<3>(tile, base, W, maxh, hl, wl, mv, mi); break;
-                    case 4: sort_scan<4>(tile, base, W, maxh, hl, wl, mv, mi); break;
-                    case 5: sort_scan<5>(tile, base, W, maxh, hl, wl, mv, mi); break;
-                    case 6: sort_scan<6>(tile, base, W, maxh, hl, wl, mv, mi); break;
-                    case 7: sort_scan<7>(tile, base, W, maxh, hl, wl, mv, mi); break;
-                    case 8: sort_scan<8>(tile, base, W, maxh, hl, wl, mv, mi); break;
-                    default: sort_scan_any(tile, base, W, maxh, maxw, hl, wl, mv, mi);
-                }
-            }
-            if (valid && !(FRCNN_SORT_X & 2)) {  // staging: one u16 code per output, [k][c][bin]
-                const int bin = ph * PW + pw;
-                uint16_t* si = reinterpret_cast<uint16_t*>(slots + slot_b * sl) + k * 8 * PHW + bin;
-#pragma unroll
-                for (int c = 0; c < 8; ++c) si[c * PHW] = static_cast<uint16_t>(empty ? 0xFFFF : mi[c] + p0 + 1);
-            }
-            ring_bump(&s_ctl[1 + sl]);
-        }
-        SPROF_MAX(3);
-        __syncthreads();  // every flush of the segment has read its slot before the table is rebuilt
-    }
-    SPROF(4);
-}
-
 // nets/heads.py:42-47 (fp32 divide, then multiply) + [idx, box] pack.
 __global__ __launch_bounds__(256) void roi_transform_kernel(const float* __restrict__ rois,
                                                             const float* __restrict__ inds,
@@ -2651,16 +2134,6 @@ extern "C" int frcnn_debug_key_prof(unsigned long long* out, int reset) {
     return 0;
 }
 #endif
-#ifdef FRCNN_SORT_PROF
-extern "C" int frcnn_debug_sort_prof(unsigned long long* out, int reset) {
-    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sort_prof), sizeof(g_sort_prof));
-    if (reset) {
-        static unsigned long long z[4096][6];
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_sort_prof), z, sizeof(z));
-    }
-    return 0;
-}
-#endif
 #ifdef FRCNN_POOL_PROF
 extern "C" int frcnn_debug_pool_prof(unsigned long long* times, unsigned* rois, int reset) {
     (void)hipMemcpyFromSymbol(times, HIP_SYMBOL(g_pool_prof), sizeof(g_pool_prof));
@@ -2894,70 +2367,15 @@ int dense_launch(const DensePlan& pl, const float* x, const float* rois, const i
     FRCNN_LAUNCH_CHECK("roi_pool_fwd_dense_kernel");
     return FRCNN_OK;
 }
-// Launch plan of the row-sorted forward: 8 channel planes per workgroup (one
-// per CU), K = 64 / PH RoIs per chunk (<= 15: the row entry is k << 4 | ph),
-// cap = RoIs per table segment from the LDS left over (<= 1024, a thread per
-// RoI); split as the wave kernel.  K = 0: does not fit (HW >= 65535: u16
-// argmax staging; C % 8; PH or PW > 15 or PH * PW > 64).
-struct SortPlan {
-    int K = 0, cap = 0, split = 1, slots = 0;
-    size_t lds = 0;
-};
-SortPlan sort_plan(int C, int N, int64_t R, int H, int W, int PH, int PW, hipStream_t st) {
-    SortPlan pl;
-    const size_t HW = static_cast<size_t>(H) * W;
-    if (N <= 0 || HW == 0 || HW >= 65535 || H > 255 || W > 255 || PH > 15 || PW > 15 || PH * PW > 64 ||
-        C % kSortCG != 0)
-        return pl;  // u16 codes, u8 windows, k << 4 | ph row entries, a wave per chunk's rows
-    constexpr size_t kReserve = 512;  // static LDS (s_red, s_ctl) + allocation rounding
-    const int K = min(64 / PH, 15);
-    const size_t slot = sort_slot_bytes(K * PH * PW);
-    const int64_t wgs = static_cast<int64_t>(C / kSortCG) * N;
-    int64_t sp = (static_cast<int64_t>(stream_cu_count(st)) + wgs - 1) / wgs;
-    if (path_cfg().roi_split > 0) sp = path_cfg().roi_split;  // A/B override
-    sp = sp < 1 ? 1 : (sp > 64 ? 64 : sp);
-    // table room for the average share + 50 % (longer shares run in segments), the rest slots
-    int64_t want = (R / N + sp - 1) / sp;
-    want = want + want / 2 + 16;
-    int cap = static_cast<int>(want < 64 ? 64 : (want > 1024 ? 1024 : want));
-    const size_t base = static_cast<size_t>(HW + 1) * 32 + kReserve;
-    while (cap > 64 && base + 3 * slot + sort_roi_bytes(cap, PH, PW) > kLdsPerCu) cap -= 16;
-    if (base + 3 * slot + sort_roi_bytes(cap, PH, PW) > kLdsPerCu) return pl;
-    int ns = static_cast<int>((kLdsPerCu - base - sort_roi_bytes(cap, PH, PW)) / slot);
-    ns = ns > kSortMaxSlots ? kSortMaxSlots : ns;
-    if (ns * slot < 2048) return pl;  // the row sort's scratch rows
-    pl.K = K;
-    pl.cap = cap;
-    pl.slots = ns;
-    pl.lds = sort_lds_bytes(static_cast<int>(HW), K, PH, PW, cap, ns);
-    pl.split = static_cast<int>(sp);
-    return pl;
-}
-
-template <bool HEAD>
-int sort_launch(const SortPlan& pl, const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
-                int PH, int PW, float ss, float* out, int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
-    const dim3 grid(static_cast<unsigned>(C / kSortCG), static_cast<unsigned>(pl.split), static_cast<unsigned>(N + 1));
-    if (PH == 7 && PW == 7)
-        hipLaunchKernelGGL((roi_pool_fwd_sort_kernel<1024, 7, HEAD>), grid, dim3(1024), pl.lds, st, x, rois,
-                           static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.K, pl.cap, pl.slots, hd);
-    else
-        hipLaunchKernelGGL((roi_pool_fwd_sort_kernel<1024, 0, HEAD>), grid, dim3(1024), pl.lds, st, x, rois,
-                           static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.K, pl.cap, pl.slots, hd);
-    FRCNN_LAUNCH_CHECK("roi_pool_fwd_sort_kernel");
-    return FRCNN_OK;
-}
-
 // One launch-plan choice for frcnn_roi_pool_fwd, frcnn_roi_pool_fwd_head and
 // the kernel-name query, so the name a caller records is the kernel launched.
-enum FwdKind { kFwdPair, kFwdKey, kFwdWave, kFwdDense, kFwdDenseList, kFwdGeneric, kFwdSort };
+enum FwdKind { kFwdPair, kFwdKey, kFwdWave, kFwdDense, kFwdDenseList, kFwdGeneric };
 struct FwdChoice {
     int kind = kFwdGeneric;
     PxPlan px;
     DensePlan dn;
-    SortPlan so;
 };
-FwdChoice choose_fwd(int64_t R, int N, int C, int H, int W, int PH, int PW, bool sorted, hipStream_t st) {
+FwdChoice choose_fwd(int N, int C, int H, int W, int PH, int PW, bool sorted, hipStream_t st) {
     FwdChoice ch;
     const int path = path_cfg().roi_fwd;
     const int PHW = PH * PW;
@@ -2972,11 +2390,7 @@ FwdChoice choose_fwd(int64_t R, int N, int C, int H, int W, int PH, int PW, bool
             ch.kind = kFwdKey;
             return ch;
         }
-        if (path == kPathSort && (ch.so = sort_plan(C, N, R, H, W, PH, PW, st)).K) {
-            ch.kind = kFwdSort;
-            return ch;
-        }
-        if ((path == kPathAuto || path == kPathWave || path == kPathPair || path == kPathKey || path == kPathSort) &&
+        if ((path == kPathAuto || path == kPathWave || path == kPathPair || path == kPathKey) &&
             (ch.px = px_plan(C, N, H, W, PHW, st)).cg) {
             ch.kind = kFwdWave;
             return ch;
@@ -2998,15 +2412,6 @@ int fwd_tile_launch(const FwdChoice& ch, const float* x, const float* rois, int6
         case kFwdPair: return pair_launch<HEAD>(ch.px, x, rois, R, N, C, H, W, PH, PW, ss, out, argmax, hd, st);
         case kFwdKey: return key_launch<HEAD>(ch.px, x, rois, R, N, C, H, W, PH, PW, ss, out, argmax, hd, st);
         case kFwdWave: return px_launch<HEAD>(ch.px, x, rois, R, N, C, H, W, PH, PW, ss, out, argmax, hd, st);
-        case kFwdSort:
-            if (reinterpret_cast<uintptr_t>(out) % 16 == 0 && reinterpret_cast<uintptr_t>(argmax) % 16 == 0)
-                return sort_launch<HEAD>(ch.so, x, rois, R, N, C, H, W, PH, PW, ss, out, argmax, hd, st);
-            {  // whole 16-B output stores need 16-B aligned outputs (every torch allocation)
-                const PxPlan px = px_plan(C, N, H, W, PH * PW, st);
-                if (px.cg) return px_launch<HEAD>(px, x, rois, R, N, C, H, W, PH, PW, ss, out, argmax, hd, st);
-            }
-            return dense_launch<HEAD, false>(dense_plan(C, N, H, W, PH * PW), x, rois, nullptr, nullptr, R, N, C, H,
-                                             W, PH, PW, ss, out, argmax, hd, st);
         default:
             return dense_launch<HEAD, false>(ch.dn, x, rois, nullptr, nullptr, R, N, C, H, W, PH, PW, ss, out,
                                              argmax, hd, st);
@@ -3030,7 +2435,7 @@ extern "C" int frcnn_roi_pool_fwd(const float* x, const float* rois, int64_t R, 
     if (R == 0 || C == 0) return FRCNN_OK;
     FRCNN_REQUIRE(x && rois && out && argmax, "frcnn_roi_pool_fwd: null pointer");
     hipStream_t st = as_stream(stream);
-    const FwdChoice ch = choose_fwd(R, N, C, H, W, PH, PW, rois_sorted != 0, st);
+    const FwdChoice ch = choose_fwd(N, C, H, W, PH, PW, rois_sorted != 0, st);
     if (ch.kind == kFwdDenseList) {  // any RoI order: per-image lists first
         FwdWs w = carve_fwd(workspace, R, N);
         FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_roi_pool_fwd: workspace %zu < %zu",
@@ -3070,7 +2475,7 @@ extern "C" int frcnn_roi_pool_fwd_kernel(int64_t R, int N, int C, int H, int W, 
     FRCNN_REQUIRE(name && len > 0, "frcnn_roi_pool_fwd_kernel: null name");
     FRCNN_REQUIRE(R >= 0 && N >= 0 && C >= 0 && H >= 0 && W >= 0 && PH > 0 && PW > 0,
                   "frcnn_roi_pool_fwd_kernel: bad shape");
-    const FwdChoice ch = choose_fwd(R, N, C, H, W, PH, PW, rois_sorted != 0, as_stream(stream));
+    const FwdChoice ch = choose_fwd(N, C, H, W, PH, PW, rois_sorted != 0, as_stream(stream));
     const int fx = PH == 7 && PW == 7 ? 7 : 0;
     // head == 2 (unaligned rois): frcnn_roi_pool_fwd_head transforms and then runs the
     // plain forward, like the dense-list / generic choices below
@@ -3083,7 +2488,6 @@ extern "C" int frcnn_roi_pool_fwd_kernel(int64_t R, int N, int C, int H, int W, 
             n = snprintf(name, len, "roi_pool_fwd_wave_kernel<1024, %d, %d, %s%s>", ch.px.cg, fx, hb,
                          path_cfg().roi_store ? ", true" : "");
             break;
-        case kFwdSort: n = snprintf(name, len, "roi_pool_fwd_sort_kernel<1024, %d, %s>", fx, hb); break;
         case kFwdDense:
             n = snprintf(name, len, "roi_pool_fwd_dense_kernel<1024, %d, %d, %s, false>", ch.dn.cg, fx, hb);
             break;
@@ -3109,7 +2513,7 @@ extern "C" int frcnn_roi_pool_fwd_head(const float* x, const float* rois, const 
     if (R == 0) return FRCNN_OK;
     FRCNN_REQUIRE(rois && roi_inds && boxes, "frcnn_roi_pool_fwd_head: null pointer");
     const bool aligned = reinterpret_cast<uintptr_t>(rois) % 16 == 0;
-    const FwdChoice ch = choose_fwd(R, N, C, H, W, PH, PW, rois_sorted != 0, as_stream(stream));
+    const FwdChoice ch = choose_fwd(N, C, H, W, PH, PW, rois_sorted != 0, as_stream(stream));
     if (!aligned || ch.kind == kFwdDenseList || ch.kind == kFwdGeneric) {
         int rc = frcnn_roi_transform(rois, roi_inds, R, img_h, img_w, H, W, boxes, stream);
         if (rc != FRCNN_OK) return rc;

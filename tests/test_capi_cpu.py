@@ -63,7 +63,7 @@ def test_set_path_accepts_the_documented_paths_only():
     accepted, anything else is rejected with rc=-1 and a message naming it."""
     from replication_faster_rcnn_amd import _lib
     lib = _lib.load(require_gpu=False)
-    ok = {"roi_pool_fwd": ["auto", "wave", "sort", "pair", "key", "dense", "generic"],
+    ok = {"roi_pool_fwd": ["auto", "wave", "pair", "key", "dense", "generic"],
           "roi_pool_bwd": ["auto", "ring", "plain"],
           "propose": ["auto", "hybrid", "lazy", "wide"],
           "roi_pool_fwd_store": ["auto", "temporal", "nt"],

@@ -249,8 +249,7 @@ def test_propose_edge_cases(case, path):
 
 
 # forward paths: (kernel path, RoIs promised grouped by image)
-FWD_PATHS = [("sort", True), ("key", True), ("wave", True), ("pair", True), ("dense", True), ("dense", False),
-             ("generic", False)]
+FWD_PATHS = [("key", True), ("wave", True), ("pair", True), ("dense", True), ("dense", False), ("generic", False)]
 
 
 def _special_x(r, N=2, C=16, H=12, W=14):
@@ -367,7 +366,7 @@ def _rand_rois(r, b, H, W, lo=-3, span=40):
     return np.concatenate([np.asarray(b, np.float32)[:, None], xy, xy + wh], 1).astype(np.float32)
 
 
-@pytest.mark.parametrize("fpath", ["sort", "key", "wave", "pair", "dense"])
+@pytest.mark.parametrize("fpath", ["key", "wave", "pair", "dense"])
 @pytest.mark.parametrize("split", ["auto", "1", "3", "64"])
 @pytest.mark.parametrize("case", ["many_images", "invalid_ends", "unsorted", "single_roi", "gaps",
                                   "one_image_tiny_rois", "uniform_sizes", "ph5", "ph8x8", "ph3x9",
