@@ -110,7 +110,7 @@ def parse():
     ap.add_argument("--roi-cg", default="auto",
                     help="channels per RoIPool forward workgroup (frcnn_set_path roi_pool_cg): auto | 4 | 8 | 16")
     ap.add_argument("--roi-path", default="auto",
-                    help="RoIPool forward kernel (frcnn_set_path roi_pool_fwd): auto | pair | wave | dense | generic")
+                    help="RoIPool forward kernel (frcnn_set_path roi_pool_fwd): auto | wave | dense | generic")
     ap.add_argument("--roi-split", default="auto",
                     help="RoI shares per (image, channel group) of the RoIPool forward "
                          "(frcnn_set_path roi_pool_split): auto | 1 | 2 | ...")

@@ -54,19 +54,17 @@ int frcnn_probe_hw_ids(uint32_t* out, int nblocks, int spin, void* stream);
 /* Kernel-path selection, process-global (tests and A/B tools; the default
  * "auto" is what every caller should use).  op / path:
  *   "roi_pool_fwd"   : "auto" | "wave" (raw image tile in LDS, compare-and-select scan, one
- *                      wave per RoI; RoIs grouped by image; the auto choice) | "key" (ordered-key
- *                      image tile, two-maximum scan) | "pair" (raw + pixel-pair tiles) | "dense"
- *                      (image tile, bins packed 64 per wave; any RoI order)
- *                      | "generic" (one workgroup per RoI)
+ *                      wave per RoI; RoIs grouped by image; the auto choice) | "dense" (image
+ *                      tile, bins packed 64 per wave; any RoI order) | "generic" (one
+ *                      workgroup per RoI)
  *   "roi_pool_bwd"   : "auto" (leader-gather plane owner for 7-wide outputs, else ring) | "ring" (latency-hidden plane owner) | "plain"
  *   "propose"        : "auto" | "hybrid" | "lazy" (fused per image) | "wide" (chip-wide bitmask)
  *   "roi_pool_split" : "auto" | "1".."64" (RoI shares per image and channel group)
  *   "roi_pool_cg"    : "auto" | "4" | "8" | "16" (channels per RoIPool forward workgroup)
  *   "roi_pool_fwd_store": "auto" = "temporal" | "nt" (the wave forward's output stores
  *                      non-temporal: better beside concurrent kernels at cfg2, worse alone)
- *   "sampler"        : "auto" | "walk" (one workgroup walks the MT19937 stream; the auto
- *                      choice) | "chip" (chip-wide chunk functions + a one-wave chain,
- *                      csrc/draws.h; the target creators' _draw / _sample entry points)
+ *   "sampler"        : "auto" | "walk" (one workgroup walks the MT19937 stream: the target
+ *                      creators' _draw / _sample entry points)
  * All paths give bit-identical results.  Not thread-safe against calls in
  * flight on other threads; set it before launching. */
 int frcnn_set_path(const char* op, const char* path);

@@ -85,8 +85,6 @@ SIGNATURES = {
 # diagnostic entry points of instrumented builds only (not in include/frcnn_capi.h)
 DEBUG_SIGNATURES = {
     "frcnn_debug_sampler_prof": (I32, [P, I32]),  # -DFRCNN_SAMPLER_PROF (tools/probe_sampler.py)
-    "frcnn_debug_key_prof": (I32, [P, I32]),      # -DFRCNN_KEY_PROF (tools/dbg/key_prof.py)
-    "frcnn_debug_draw_hdr": (I32, [I32, I32, I32, I32, I32, P, P]),  # tools/probe_draws.py
 }
 
 _lib = None

@@ -67,12 +67,9 @@ extern "C" int frcnn_set_path(const char* op, const char* path) {
     auto is = [&](const char* a, const char* b) { return std::strcmp(a, b) == 0; };
     const bool aut = is(path, "auto");
     if (is(op, "roi_pool_fwd") &&
-        (aut || is(path, "pair") || is(path, "wave") || is(path, "key") || is(path, "dense") ||
-         is(path, "generic"))) {
+        (aut || is(path, "wave") || is(path, "dense") || is(path, "generic"))) {
         g_path.roi_fwd = aut ? kPathAuto : is(path, "generic") ? kPathGeneric
                                        : is(path, "dense")     ? kPathDense
-                                       : is(path, "pair")      ? kPathPair
-                                       : is(path, "key")       ? kPathKey
                                                                : kPathWave;
     } else if (is(op, "roi_pool_bwd") &&
                (aut || is(path, "ring") || is(path, "plain"))) {
@@ -84,8 +81,8 @@ extern "C" int frcnn_set_path(const char* op, const char* path) {
                                                               : kPathWide;
     } else if (is(op, "roi_pool_fwd_store") && (aut || is(path, "temporal") || is(path, "nt"))) {
         g_path.roi_store = is(path, "nt") ? 1 : 0;
-    } else if (is(op, "sampler") && (aut || is(path, "walk") || is(path, "chip"))) {
-        g_path.sampler = aut ? kPathAuto : is(path, "walk") ? kPathWalk : kPathChip;
+    } else if (is(op, "sampler") && (aut || is(path, "walk"))) {
+        g_path.sampler = aut ? kPathAuto : kPathWalk;
     } else if (is(op, "roi_pool_split")) {
         char* end = nullptr;
         const long v = aut ? 0 : std::strtol(path, &end, 10);

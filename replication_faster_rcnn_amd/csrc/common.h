@@ -19,15 +19,12 @@ constexpr int kPathAuto = 0;
 constexpr int kPathGeneric = 1;  // roi_pool_fwd: one workgroup per RoI
 constexpr int kPathDense = 2;    // roi_pool_fwd: image tile, RoI bins packed per wave
 constexpr int kPathWave = 3;     // roi_pool_fwd: image tile, one wave per RoI (RoIs grouped by image)
-constexpr int kPathPair = 4;     // roi_pool_fwd: raw + pixel-pair tiles, one wave per RoI (grouped by image)
-constexpr int kPathKey = 5;      // roi_pool_fwd: ordered-key tile, two-maximum scan, one wave per RoI (grouped by image)
 constexpr int kPathPlain = 1;    // roi_pool_bwd: the unpipelined plane-owner kernel
 constexpr int kPathRing = 2;     // roi_pool_bwd: the RoI-at-a-time ring kernel (auto: leader kernel)
 constexpr int kPathHybrid = 1;   // propose: fused per image + chip-wide first-chunk mask
 constexpr int kPathLazy = 2;     // propose: fused per image, lazy NMS from the first chunk on
 constexpr int kPathWide = 3;     // propose: chip-wide sort + bitmask NMS
 constexpr int kPathWalk = 1;     // sampler: one workgroup walks the MT19937 stream (auto)
-constexpr int kPathChip = 2;     // sampler: chip-wide chunk functions + a one-wave chain (draws.h)
 struct PathCfg {
     int roi_fwd = kPathAuto;
     int roi_bwd = kPathAuto;

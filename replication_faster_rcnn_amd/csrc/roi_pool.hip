@@ -766,598 +766,6 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
     PPROF_T(3);
 }
 
-// ------------------------------------------------- pair-tile forward
-// The default forward for RoIs grouped by image when the tiles fit the CU's
-// LDS.  Same grid and RoI shares as the wave kernel, but the workgroup stages
-// TWO tiles of its CG channel planes: the raw pixels and the horizontal pixel
-// PAIRS -- pair (h, w) = the first maximum of pixels (h, w), (h, w+1) under
-// torchvision's strict '>' (NaN never selected), plus one flag bit per channel
-// saying whether it is the second pixel.  A lane (= one bin) scans each window
-// row as pairs at columns ws, ws+2, ..., the last one clamped to we-2 (a pair
-// seen twice can never pass the strict '>' again); 1-wide windows read the raw
-// tile.  Scanning pairs in row-major order picks the same first maximum as
-// scanning pixels: the first pair holding the overall maximum holds its first
-// occurrence, and a tie inside the pair goes to its first pixel.  So a window
-// row of width w takes ceil(w/2) updates instead of w, each the same compare +
-// two selects per channel; the update records X = (pair pixel << 16) | flags
-// and the argmax is decoded once after the scan (pixel + this channel's flag).
-// Staging the pairs costs one compare per pixel-channel per workgroup against
-// ~47 window visits of each pixel-channel at cfg2.
-// Lanes: one bin each; for the 7x7 head the lane -> bin map puts two whole
-// bin rows into each of the four 16-lane groups a ds_read_b128 is serviced in
-// (fewer bank conflicts than consecutive bins: rows of one bin row share the
-// pixel row).  Waves pull RoIs from an LDS counter; the chunk prologue
-// computes each RoI's geometry once per workgroup, with its largest bin height
-// and pair count (the wave-uniform loop bounds).
-__constant__ signed char kPairLaneBin7[64] = {
-    0,  1,  2,  3,  14, 15, 16, 17, 18, 19, 20, 21, 4,  5,  6,  7,  22, 23, 24, 25, 8,  9,
-    10, 11, 12, 13, -1, -1, 26, 27, -1, -1, 28, 29, 30, 31, 42, 43, 44, 45, 46, 47, 48, -1,
-    32, 33, 34, 35, -1, -1, -1, -1, 36, 37, 38, 39, 40, 41, -1, -1, -1, -1, -1, -1};
-
-__host__ __device__ constexpr int pair_hws(int HW) { return (HW + 16) & ~15; }  // + the sentinel pixel HW
-
-template <int NT, int CG, int FIX, bool HEAD>
-__global__ __launch_bounds__(NT) void roi_pool_fwd_pair_kernel(
-    const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W, int PH_, int PW_,
-    float ss, float* __restrict__ out, int32_t* __restrict__ argmax, int geo_cap, HeadArgs hd) {
-    const int PH = FIX ? FIX : PH_, PW = FIX ? FIX : PW_;
-    constexpr int NP = CG / 4;
-    static_assert(CG <= 8, "8 flag bits per pixel word");
-    extern __shared__ __attribute__((aligned(16))) float4 q4[];
-    __shared__ int s_red[2 * (NT / 64)];
-    __shared__ int s_next;
-    const int b = blockIdx.z;
-    const int c0 = blockIdx.x * CG;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int HW = H * W;
-    const int HWs = pair_hws(HW);
-    const int PHW = PH * PW;
-    const int split = gridDim.y, z = blockIdx.y;
-    const int N = gridDim.z - 1;
-    if (b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
-        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, 0, N, s_red, 1)
-                             : roi_range_sorted<NT>(rois, R, 0, N, s_red);
-        const int n_lo = rg.x, tot = n_lo + (R - rg.y);
-        const int lo = static_cast<int>(static_cast<int64_t>(tot) * z / split);
-        const int hi = static_cast<int>(static_cast<int64_t>(tot) * (z + 1) / split);
-        if (HEAD && hd.boxes && blockIdx.x == 0)
-            for (int t = lo + tid; t < hi; t += NT) {
-                const int r = t < n_lo ? t : rg.y + (t - n_lo);
-                float bx[5];
-                head_box(rois, hd, r, bx);
-#pragma unroll
-                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
-            }
-        for (int e = lo * CG * PHW + tid; e < hi * CG * PHW; e += NT) {
-            const int t = e / (CG * PHW);
-            const int rem = e - t * (CG * PHW);
-            const int r = t < n_lo ? t : rg.y + (t - n_lo);
-            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + rem;
-            out[o] = 0.0f;
-            argmax[o] = -1;
-        }
-        return;
-    }
-    const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, b, b + 1, s_red, 1)
-                         : roi_range_sorted<NT>(rois, R, b, b + 1, s_red);
-    const int rbase = rg.x, nr = rg.y - rg.x;
-    if (z >= nr) return;
-    const int nmine = (nr - z + split - 1) / split;  // items z, z+split, ...
-    // ---- LDS: raw planes | pair planes | flags | RoI geometry | loop bounds
-    float4* raw = q4;
-    float4* prt = q4 + NP * HWs;
-    uint16_t* flw = reinterpret_cast<uint16_t*>(q4 + 2 * NP * HWs);
-    int4* s_geo = reinterpret_cast<int4*>(flw + HWs);  // HWs is a multiple of 16
-    int* s_ext = reinterpret_cast<int*>(s_geo + geo_cap);
-    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
-    for (int p = tid; p < HW; p += NT) {
-        float v[CG];
-#pragma unroll
-        for (int q = 0; q < CG; ++q) v[q] = src[static_cast<size_t>(q) * HW + p];
-#pragma unroll
-        for (int k = 0; k < NP; ++k) raw[k * HWs + p] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
-    }
-    for (int p = HW + tid; p < HWs; p += NT)  // the sentinel pixel HW and the padding: -inf
-#pragma unroll
-        for (int k = 0; k < NP; ++k) raw[k * HWs + p] = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-    __syncthreads();
-    // pairs + flag words: flw[p] = (w << 8) | flags (bit c: channel c's pair
-    // maximum is the second pixel), so a scan step's index record is its row's
-    // (h * W) << 8 plus this word; the sentinel's word is 0
-    for (int p = tid; p < HWs; p += NT) {
-        const int row = p / W;
-        const int w = p - row * W;
-        const bool two = p < HW && w != W - 1;  // pixel (h, w+1) exists
-        uint32_t fl = 0;
-#pragma unroll
-        for (int k = 0; k < NP; ++k) {
-            const float4 a4 = raw[k * HWs + p];
-            const float4 b4 = raw[k * HWs + (two ? p + 1 : p)];
-            const float a[4] = {a4.x, a4.y, a4.z, a4.w};
-            const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
-            float o[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                // the pixel a strict-'>' scan of (a, b) from -FLT_MAX keeps: b iff
-                // b > a, or a is NaN (never selected) -- then b, NaN or not
-                const bool tb = two && (bb[j] > a[j] || a[j] != a[j]);
-                o[j] = tb ? bb[j] : a[j];
-                fl |= static_cast<uint32_t>(tb) << (4 * k + j);
-            }
-            prt[k * HWs + p] = make_float4(o[0], o[1], o[2], o[3]);
-        }
-        flw[p] = static_cast<uint16_t>(p < HW ? (w << 8) | fl : 0);
-    }
-    const int bin = FIX == 7 ? static_cast<int>(kPairLaneBin7[lane]) : (lane < PHW ? lane : -1);
-    const bool act = bin >= 0;
-    const int ph = act ? bin / PW : 0, pw = act ? bin - (bin / PW) * PW : 0;
-    const char* tb = reinterpret_cast<const char*>(q4);  // byte offsets below
-    const uint32_t plane_bytes = static_cast<uint32_t>(HWs) * 16u;
-    const uint32_t raw_b = 0, prt_b = NP * plane_bytes, flw_b = 2 * NP * plane_bytes;
-    for (int k0 = 0; k0 < nmine; k0 += geo_cap) {
-        const int cn = min(geo_cap, nmine - k0);
-        for (int i = tid; i < cn; i += NT) {
-            const int r = rbase + z + (k0 + i) * split;
-            float bx[5];
-            if (HEAD) {
-                head_box(rois, hd, r, bx);
-                if (hd.boxes && blockIdx.x == 0) {
-#pragma unroll
-                    for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 5; ++j) bx[j] = rois[static_cast<size_t>(r) * 5 + j];
-            }
-            const RoiGeom gm = roi_geom(bx, ss, PH, PW);
-            s_geo[i] = make_int4(gm.sh, gm.sw, __float_as_int(gm.bh), __float_as_int(gm.bw));
-            // wave-uniform loop bounds: the largest bin height and pair count
-            int hm = 0, um = 0;
-            for (int q = 0; q < PH; ++q) {
-                const int4 g = geom_bin(gm, H, W, q, 0);
-                hm = max(hm, g.y - g.x);
-            }
-            for (int q = 0; q < PW; ++q) {
-                const int4 g = geom_bin(gm, H, W, 0, q);
-                const int w = g.w - g.z;
-                um = max(um, w <= 0 ? 0 : (w == 1 ? 1 : (w + 1) >> 1));
-            }
-            s_ext[i] = (hm << 16) | um;
-        }
-        if (tid == 0) s_next = 0;
-        __syncthreads();  // tiles staged (first chunk) / geometry of the chunk
-        int k = 0;
-        if (lane == 0) k = atomicAdd(&s_next, 1);
-        k = __builtin_amdgcn_readfirstlane(k);
-        while (k < cn) {
-            int kn = 0;
-            if (lane == 0) kn = atomicAdd(&s_next, 1);  // prefetch the next item
-            const int r = rbase + z + (k0 + k) * split;
-            const int4 gq = s_geo[k];
-            const int ext = __builtin_amdgcn_readfirstlane(s_ext[k]);
-            const int Hm = ext >> 16, Um = ext & 0xffff;
-            RoiGeom gm;
-            gm.sh = gq.x;
-            gm.sw = gq.y;
-            gm.bh = __int_as_float(gq.z);
-            gm.bw = __int_as_float(gq.w);
-            const int4 g = geom_bin(gm, H, W, ph, pw);
-            const int ww = g.w - g.z;
-            const bool empty = !act || g.y <= g.x || ww <= 0;
-            const int hh = empty ? 0 : g.y - g.x;
-            const bool single = ww == 1;
-            const int last = max(ww - 2, 0);  // start of a row's last pair (0: 1-wide, raw tile)
-            const uint32_t tbase = single ? raw_b : prt_b;
-            float m[CG];
-            int X[CG];
-#pragma unroll
-            for (int c = 0; c < CG; ++c) {
-                m[c] = empty ? 0.0f : -FLT_MAX;
-                X[c] = static_cast<int>(0xFFFFFF00u);  // decodes to -1
-            }
-            int rowpix = g.x * W + g.z;
-            for (int i = 0; i < Hm; ++i) {
-                if (i < hh) {
-                    const uint32_t ra0 = tbase + static_cast<uint32_t>(rowpix) * 16u;
-                    const uint32_t ra1 = ra0 + plane_bytes;
-                    // 1-wide windows read the sentinel's word 0: their one pixel is "first"
-                    const uint32_t fra = flw_b + 2u * static_cast<uint32_t>(single ? HW : rowpix);
-                    const int rowX = (rowpix - g.z) << 8;  // (h * W) << 8
-                    const int rowXs = single ? (rowpix << 8) : rowX;
-                    for (int j = 0; j < Um; ++j) {
-                        const uint32_t q = static_cast<uint32_t>(min(2 * j, last));
-                        const float4 v0 = *static_cast<const float4*>(__builtin_assume_aligned(tb + ra0 + q * 16u, 16));
-                        float4 v1 = v0;
-                        if (NP > 1) v1 = *static_cast<const float4*>(__builtin_assume_aligned(tb + ra1 + q * 16u, 16));
-                        const uint32_t fw = *reinterpret_cast<const uint16_t*>(tb + fra + 2u * q);
-                        // every read in flight before the first compare
-                        __builtin_amdgcn_sched_barrier(0);
-                        const int xn = rowXs + static_cast<int>(fw);
-                        const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-#pragma unroll
-                        for (int c = 0; c < CG; ++c) {
-                            if (vv[c] > m[c]) {  // torchvision's strict '>'
-                                m[c] = vv[c];
-                                X[c] = xn;
-                            }
-                        }
-                    }
-                }
-                rowpix += W;
-            }
-            if (act) {
-                const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + bin;
-                float* op = out + o;
-                int32_t* ap = argmax + o;
-#pragma unroll
-                for (int c = 0; c < CG; ++c) {
-                    op[c * PHW] = m[c];
-                    ap[c * PHW] = (X[c] >> 8) + ((X[c] >> c) & 1);
-                }
-            }
-            k = __builtin_amdgcn_readfirstlane(kn);
-        }
-        __syncthreads();  // the chunk's geometry and s_next are reused
-    }
-}
-
-// ------------------------------------------------- ordered-key forward
-// pool_key: a bijection of the fp32 bit patterns onto u32 that orders the
-// non-NaN floats like '<' (sign-magnitude -> offset binary), plus one, so that
-// -0.0 (key 0x80000000) and +0.0 (0x80000001) fall into the same key class
-// (keys equal above the low kKeyBits bits).  NaN / -inf / -FLT_MAX are never
-// selected by torchvision's strict '>' against -FLT_MAX; a workgroup whose
-// planes hold any of them takes the exact scan (key_exact) for all its RoIs.
-#ifdef FRCNN_KEY_PROF
-__device__ unsigned long long g_key_prof[4];  // fast RoI-waves, re-scanning waves, re-scanned lanes, exact RoI-waves
-#define KPROF(i, v) do { if (lane == 0) atomicAdd(&g_key_prof[i], static_cast<unsigned long long>(v)); } while (0)
-#else
-#define KPROF(i, v) do {} while (0)
-#endif
-#ifndef FRCNN_KEY_DBG
-#define FRCNN_KEY_DBG 0  // experiment builds only: 1 no check, 2 no K pass, 4 no stores, 8 fake check
-#endif
-#ifndef FRCNN_KEY_NT
-#define FRCNN_KEY_NT 1024
-#endif
-constexpr int kKeyNT = FRCNN_KEY_NT;  // threads per key-kernel workgroup
-constexpr int kKeyBits = 10;
-constexpr uint32_t kKeyMask = (1u << kKeyBits) - 1;
-constexpr uint32_t kKeyZero = 0x80000001u;  // pool_key(+0.0f): the empty-window sentinel
-
-__device__ __forceinline__ uint32_t pool_key(float v) {
-    const uint32_t u = __float_as_uint(v);
-    return (u ^ (static_cast<uint32_t>(static_cast<int32_t>(u) >> 31) | 0x80000000u)) + 1u;
-}
-// (key & ~kKeyMask) | code as one v_bitop3_b32 (truth table 0xDC on
-// (key, code, mask)): measured 2.7 cycles per wave64 instruction at 4 waves per
-// SIMD against 4.7 for v_and_or_b32 (tools/valu_rate2.hip).
-__device__ __forceinline__ uint32_t key_code(uint32_t key, uint32_t code, uint32_t low_mask) {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xdc" : "=v"(r) : "v"(key), "v"(code), "s"(low_mask));
-    return r;
-}
-__device__ __forceinline__ uint32_t pool_unkey(uint32_t k) {
-    const uint32_t u = k - 1u;
-    return u ^ (~static_cast<uint32_t>(static_cast<int32_t>(u) >> 31) | 0x80000000u);
-}
-
-// torchvision's exact window scan (strict '>' from -FLT_MAX, row-major first
-// maximum, empty window -> 0 / -1) over the key tile, CG channels at once.
-template <int NP>
-__device__ __forceinline__ void key_exact(const uint4* __restrict__ k4, int p0, int hh, int ww, int W,
-                                          float (&mv)[4 * NP], int (&mi)[4 * NP]) {
-    const float init = (hh <= 0 || ww <= 0) ? 0.0f : -FLT_MAX;
-#pragma unroll
-    for (int c = 0; c < 4 * NP; ++c) {
-        mv[c] = init;
-        mi[c] = -1;
-    }
-    for (int dh = 0; dh < hh; ++dh) {
-        for (int dw = 0; dw < ww; ++dw) {
-            const int p = p0 + dh * W + dw;
-            const uint4* pp = reinterpret_cast<const uint4*>(tile_px<NP>(reinterpret_cast<const float4*>(k4), p));
-#pragma unroll
-            for (int q = 0; q < NP; ++q) {
-                const uint4 t = pp[16 * q];
-                const uint32_t tt[4] = {t.x, t.y, t.z, t.w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float v = __uint_as_float(pool_unkey(tt[j]));
-                    if (v > mv[4 * q + j]) {
-                        mv[4 * q + j] = v;
-                        mi[4 * q + j] = p;
-                    }
-                }
-            }
-        }
-    }
-}
-
-// The default forward for RoIs grouped by image.  Grid, RoI shares, the LDS
-// RoI counter and the per-chunk geometry are the wave kernel's (one wave per
-// RoI, lane = bin, CG channels per lane); the tile holds pool_key(x) instead of
-// x, and the scan replaces torchvision's compare + two selects per
-// pixel-channel with two u32 maxima and one and-or:
-//   M = max over the window of key           (the maximum, exactly)
-//   K = max over the window of (key & ~mask) | (mask - (p - p0))
-// K's class is M's class, and among the window's pixels of that class K names
-// the first in row-major order (p - p0 grows with it).  If that pixel's value
-// is M, it is the first pixel holding the maximum: torchvision's answer, and
-// the output value is pool_unkey(M) (bit-exact incl. the sign of a zero).  The
-// check reads the named pixel's key from the tile; a lane whose check fails
-// for any channel (another value of the same class precedes the maximum, e.g.
-// -0.0 before +0.0: rare) re-scans its window exactly.
-// Loops are wave-uniform over the RoI's largest bin (hmax x wmax, from the
-// chunk prologue), each lane's pixel clamped into its own window (re-reading a
-// pixel changes neither maximum), two pixels per step (v_max3_u32).
-template <int NT, int CG, int FIX, bool HEAD>
-__global__ __launch_bounds__(NT) void roi_pool_fwd_key_kernel(
-    const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W, int PH_, int PW_,
-    float ss, float* __restrict__ out, int32_t* __restrict__ argmax, int geo_cap, HeadArgs hd) {
-    const int PH = FIX ? FIX : PH_, PW = FIX ? FIX : PW_;
-    constexpr int NP = CG / 4;
-    extern __shared__ __attribute__((aligned(16))) uint4 k4[];  // key tile (tile_px layout); geometry after
-    __shared__ int s_red[2 * (NT / 64)];
-    __shared__ int s_next;
-    const int b = blockIdx.z;
-    const int c0 = blockIdx.x * CG;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int HW = H * W;
-    const int HWs = (HW + 16) & ~15;  // + the zero sentinel pixel HW
-    const int PHW = PH * PW;
-    const int split = gridDim.y, z = blockIdx.y;
-    const int N = gridDim.z - 1;
-    PPROF_T(0);
-    if (b == N) {  // out-of-range batch indices: [0, count(<0)) and [count(<N), R)
-        const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, 0, N, s_red, 1)
-                             : roi_range_sorted<NT>(rois, R, 0, N, s_red);
-        const int n_lo = rg.x, tot = n_lo + (R - rg.y);
-        const int lo = static_cast<int>(static_cast<int64_t>(tot) * z / split);
-        const int hi = static_cast<int>(static_cast<int64_t>(tot) * (z + 1) / split);
-        if (HEAD && hd.boxes && blockIdx.x == 0)
-            for (int t = lo + tid; t < hi; t += NT) {
-                const int r = t < n_lo ? t : rg.y + (t - n_lo);
-                float bx[5];
-                head_box(rois, hd, r, bx);
-#pragma unroll
-                for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
-            }
-        for (int e = lo * CG * PHW + tid; e < hi * CG * PHW; e += NT) {
-            const int t = e / (CG * PHW);
-            const int rem = e - t * (CG * PHW);
-            const int r = t < n_lo ? t : rg.y + (t - n_lo);
-            const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + rem;
-            out[o] = 0.0f;
-            argmax[o] = -1;
-        }
-        return;
-    }
-    const int2 rg = HEAD ? roi_range_sorted<NT>(hd.inds, R, b, b + 1, s_red, 1)
-                         : roi_range_sorted<NT>(rois, R, b, b + 1, s_red);
-    const int rbase = rg.x, nr = rg.y - rg.x;
-    PPROF_T(1);
-    if (z >= nr) return;
-    const int nmine = (nr - z + split - 1) / split;  // items z, z+split, ...
-    PPROF_ROIS(nmine);
-    const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
-    const float4* t4 = reinterpret_cast<const float4*>(k4);
-    if (tid < NP) {
-        uint4* s = const_cast<uint4*>(reinterpret_cast<const uint4*>(tile_px<NP>(t4, HW)));
-        s[16 * tid] = make_uint4(kKeyZero, kKeyZero, kKeyZero, kKeyZero);
-    }
-    int special = 0;
-    for (int p = tid; p < HW; p += NT) {
-        uint32_t v[CG];
-#pragma unroll
-        for (int q = 0; q < CG; ++q) {
-            const float e = src[static_cast<size_t>(q) * HW + p];
-            special |= !(e > -FLT_MAX);  // NaN, -inf, -FLT_MAX
-            v[q] = pool_key(e);
-        }
-        uint4* pp = const_cast<uint4*>(reinterpret_cast<const uint4*>(tile_px<NP>(t4, p)));
-#pragma unroll
-        for (int k = 0; k < NP; ++k) pp[16 * k] = make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
-    }
-    special = __syncthreads_or(special);
-    int4* s_geo = reinterpret_cast<int4*>(k4 + NP * HWs);
-    int* s_ext = reinterpret_cast<int*>(s_geo + geo_cap);  // hmax | wmax << 16
-    const int ph = lane / PW, pw = lane - (lane / PW) * PW;
-    const bool act = lane < PHW;
-    for (int k0 = 0; k0 < nmine; k0 += geo_cap) {
-        const int cn = min(geo_cap, nmine - k0);
-        for (int i = tid; i < cn; i += NT) {
-            const int r = rbase + z + (k0 + i) * split;
-            float bx[5];
-            if (HEAD) {
-                head_box(rois, hd, r, bx);
-                if (hd.boxes && blockIdx.x == 0) {
-#pragma unroll
-                    for (int j = 0; j < 5; ++j) hd.boxes[static_cast<size_t>(r) * 5 + j] = bx[j];
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 5; ++j) bx[j] = rois[static_cast<size_t>(r) * 5 + j];
-            }
-            const RoiGeom gm = roi_geom(bx, ss, PH, PW);
-            int hm = 1, wm = 1;
-            for (int t = 0; t < PH; ++t) {
-                const int4 gb = geom_bin(gm, H, W, t, 0);
-                hm = max(hm, gb.y - gb.x);
-            }
-            for (int t = 0; t < PW; ++t) {
-                const int4 gb = geom_bin(gm, H, W, 0, t);
-                wm = max(wm, gb.w - gb.z);
-            }
-            s_geo[i] = make_int4(gm.sh, gm.sw, __float_as_int(gm.bh), __float_as_int(gm.bw));
-            s_ext[i] = hm | (wm << 16);
-        }
-        if (tid == 0) s_next = 0;
-        __syncthreads();
-        if (k0 == 0) PPROF_T(2);
-        // paced output: RoI t-1's 2*CG stores go out 4 at a time between RoI t's
-        // scan steps (kPace), so the store queue is fed evenly instead of in
-        // 32-store bursts the waves would all wait behind
-        constexpr bool kPace = (FRCNN_KEY_DBG & 32) != 0;
-        constexpr int kBlk = CG / 2;
-        float pv[CG];
-        uint32_t pi2[CG / 2];  // argmax pairs, 16 bits each (|argmax| < H * W + 1 <= 32768)
-        size_t po = 0;
-        int pblk = kBlk;  // blocks of the pending RoI not yet stored (kBlk: none pending)
-        auto pace = [&](int bb_) {
-            if (act) {
-                float* op = out + po;
-                int32_t* ap = argmax + po;
-#pragma unroll
-                for (int bb = 0; bb < kBlk; ++bb)
-                    if (bb == bb_) {
-                        op[(2 * bb) * PHW] = pv[2 * bb];
-                        ap[(2 * bb) * PHW] = static_cast<int>(static_cast<int16_t>(pi2[bb] & 0xFFFFu));
-                        op[(2 * bb + 1) * PHW] = pv[2 * bb + 1];
-                        ap[(2 * bb + 1) * PHW] = static_cast<int>(pi2[bb]) >> 16;
-                    }
-            }
-        };
-        int k = 0;
-        if (lane == 0) k = atomicAdd(&s_next, 1);
-        k = __builtin_amdgcn_readfirstlane(k);
-        while (k < cn) {
-            int kn = 0;
-            if (lane == 0) kn = atomicAdd(&s_next, 1);  // prefetch the next item
-            const int r = rbase + z + (k0 + k) * split;
-            const int4 gq = s_geo[k];
-            const int ex = __builtin_amdgcn_readfirstlane(s_ext[k]);
-            const int hmax = ex & 0xFFFF, wmax = ex >> 16;
-            RoiGeom gm;
-            gm.sh = gq.x;
-            gm.sw = gq.y;
-            gm.bh = __int_as_float(gq.z);
-            gm.bw = __int_as_float(gq.w);
-            int4 g = geom_bin(gm, H, W, ph, pw);
-            if (!act) g = make_int4(0, 0, 0, 0);
-            const bool empty = g.y <= g.x || g.w <= g.z;
-            const int p0 = empty ? HW : g.x * W + g.z;
-            float val[CG];
-            int idx[CG];
-            if (special || (hmax - 1) * W + (wmax - 1) > static_cast<int>(kKeyMask)) {
-                KPROF(3, 1);
-                key_exact<NP>(k4, p0, empty ? 0 : g.y - g.x, empty ? 0 : g.w - g.z, W, val, idx);
-            } else {
-                KPROF(0, 1);
-                const int hh1 = empty ? 0 : g.y - g.x - 1, ww1 = empty ? 0 : g.w - g.z - 1;
-                const uint32_t cb = static_cast<uint32_t>(p0) + kKeyMask;
-                const uint32_t kmask = __builtin_amdgcn_readfirstlane(kKeyMask);  // SGPR operand of key_code
-                uint32_t K[CG], M[CG];
-#pragma unroll
-                for (int c = 0; c < CG; ++c) K[c] = M[c] = 0u;
-                for (int dh = 0; dh < hmax; ++dh) {
-                    const int rb = p0 + min(dh, hh1) * W;
-                    int dw = 0;
-                    for (; dw + 1 < wmax; dw += 2) {  // two pixels per step
-                        const int pa = rb + min(dw, ww1), pb = rb + min(dw + 1, ww1);
-                        const uint4* qa = reinterpret_cast<const uint4*>(tile_px<NP>(t4, pa));
-                        const uint4* qb = reinterpret_cast<const uint4*>(tile_px<NP>(t4, pb));
-                        uint4 va[NP], vb[NP];
-#pragma unroll
-                        for (int q = 0; q < NP; ++q) {
-                            va[q] = qa[16 * q];
-                            vb[q] = qb[16 * q];
-                        }
-                        __builtin_amdgcn_sched_barrier(0);
-                        const uint32_t ca = cb - static_cast<uint32_t>(pa), cc = cb - static_cast<uint32_t>(pb);
-#pragma unroll
-                        for (int q = 0; q < NP; ++q) {
-                            const uint32_t ta[4] = {va[q].x, va[q].y, va[q].z, va[q].w};
-                            const uint32_t tb[4] = {vb[q].x, vb[q].y, vb[q].z, vb[q].w};
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) {
-                                const uint32_t ka = key_code(ta[j], ca, kmask), kb = key_code(tb[j], cc, kmask);
-                                if (!(FRCNN_KEY_DBG & 2)) K[4 * q + j] = max(K[4 * q + j], max(ka, kb));
-                                M[4 * q + j] = max(M[4 * q + j], max(ta[j], tb[j]));
-                            }
-                        }
-                        if (kPace && pblk < kBlk) pace(pblk++);
-                    }
-                    if (dw < wmax) {  // odd width: the last column alone
-                        const int pa = rb + min(dw, ww1);
-                        const uint4* qa = reinterpret_cast<const uint4*>(tile_px<NP>(t4, pa));
-                        uint4 va[NP];
-#pragma unroll
-                        for (int q = 0; q < NP; ++q) va[q] = qa[16 * q];
-                        __builtin_amdgcn_sched_barrier(0);
-                        const uint32_t ca = cb - static_cast<uint32_t>(pa);
-#pragma unroll
-                        for (int q = 0; q < NP; ++q) {
-                            const uint32_t ta[4] = {va[q].x, va[q].y, va[q].z, va[q].w};
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) {
-                                if (!(FRCNN_KEY_DBG & 2)) K[4 * q + j] = max(K[4 * q + j], key_code(ta[j], ca, kmask));
-                                M[4 * q + j] = max(M[4 * q + j], ta[j]);
-                            }
-                        }
-                        if (kPace && pblk < kBlk) pace(pblk++);
-                    }
-                }
-                // the first pixel of the maximum's class and the check of its key
-                // against the maximum (LDS: a reload from memory would wait, in
-                // vmcnt order, for the previous RoI's stores); an empty window
-                // names the sentinel pixel (key +0.0 = its maximum) and argmax -1
-                // (ds_read_b128 of the named pixel's 4-channel quad: its 16-B slots
-                // spread over all 64 banks; a dword read of one channel would hit
-                // 8 of 32 banks)
-                const int ioff = empty ? -(HW + 1) : 0;
-                uint32_t bad = 0;
-#pragma unroll
-                for (int c = 0; c < CG; ++c) {
-                    const int p = static_cast<int>(cb - (K[c] & kKeyMask));
-                    idx[c] = p + ioff;
-                    if (FRCNN_KEY_DBG & 8) bad |= K[c] == 0xFFFFFFFFu;  // experiment: keep the re-scan, no reads
-                    if (!(FRCNN_KEY_DBG & 9)) {
-                        const uint4 t4q = reinterpret_cast<const uint4*>(tile_px<NP>(t4, p))[16 * (c / 4)];
-                        const uint32_t t = (c % 4) == 0 ? t4q.x : (c % 4) == 1 ? t4q.y : (c % 4) == 2 ? t4q.z : t4q.w;
-                        bad |= t ^ M[c];
-                    }
-                    val[c] = __uint_as_float(pool_unkey(M[c]));
-                }
-                if (__builtin_amdgcn_ballot_w64(bad != 0)) {
-                    KPROF(1, 1);
-                    { const auto bl = __builtin_amdgcn_ballot_w64(bad != 0); KPROF(2, __builtin_popcountll(bl)); }
-                    if (bad) key_exact<NP>(k4, p0, empty ? 0 : g.y - g.x, empty ? 0 : g.w - g.z, W, val, idx);
-                }
-            }
-            if (kPace) {
-                while (pblk < kBlk) pace(pblk++);
-#pragma unroll
-                for (int c = 0; c < CG; ++c) pv[c] = val[c];
-#pragma unroll
-                for (int c = 0; c < CG / 2; ++c)
-                    pi2[c] = (static_cast<uint32_t>(idx[2 * c]) & 0xFFFFu) | (static_cast<uint32_t>(idx[2 * c + 1]) << 16);
-                po = (static_cast<size_t>(r) * C + c0) * PHW + lane;
-                pblk = 0;
-            } else if (act && !(FRCNN_KEY_DBG & 4)) {
-                const size_t o = (static_cast<size_t>(r) * C + c0) * PHW + lane;
-                float* op = out + o;
-                int32_t* ap = argmax + o;
-#pragma unroll
-                for (int c = 0; c < CG; ++c) {
-                    if (FRCNN_KEY_DBG & 16) {
-                        __builtin_nontemporal_store(val[c], op + c * PHW);
-                        __builtin_nontemporal_store(idx[c], ap + c * PHW);
-                    } else {
-                        op[c * PHW] = val[c];
-                        ap[c * PHW] = idx[c];
-                    }
-                }
-            }
-            k = __builtin_amdgcn_readfirstlane(kn);
-        }
-        if (kPace)
-            while (pblk < kBlk) pace(pblk++);
-        __syncthreads();  // the chunk's geometry and s_next are reused
-    }
-    PPROF_T(3);
-}
-
 // nets/heads.py:42-47 (fp32 divide, then multiply) + [idx, box] pack.
 __global__ __launch_bounds__(256) void roi_transform_kernel(const float* __restrict__ rois,
                                                             const float* __restrict__ inds,
@@ -2124,16 +1532,6 @@ extern "C" int frcnn_debug_bwd_prof(unsigned long long* out, int reset) {
     return 0;
 }
 #endif
-#ifdef FRCNN_KEY_PROF
-extern "C" int frcnn_debug_key_prof(unsigned long long* out, int reset) {
-    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_key_prof), sizeof(g_key_prof));
-    if (reset) {
-        unsigned long long z[4] = {};
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_key_prof), z, sizeof(z));
-    }
-    return 0;
-}
-#endif
 #ifdef FRCNN_POOL_PROF
 extern "C" int frcnn_debug_pool_prof(unsigned long long* times, unsigned* rois, int reset) {
     (void)hipMemcpyFromSymbol(times, HIP_SYMBOL(g_pool_prof), sizeof(g_pool_prof));
@@ -2226,87 +1624,6 @@ int px_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, in
     return FRCNN_OK;
 }
 
-// The ordered-key forward: the wave kernel's plan with 20 B of geometry per RoI.
-PxPlan key_plan(int C, int N, int H, int W, int PHW, hipStream_t st) {
-    return px_plan(C, N, H, W, PHW, st, sizeof(int4) + sizeof(int));
-}
-
-template <bool HEAD>
-int key_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
-               int PH, int PW, float ss, float* out, int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
-    const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(pl.split), static_cast<unsigned>(N + 1));
-    const bool fix7 = PH == 7 && PW == 7;
-#define FRCNN_KEY(CG, FX)                                                                                  \
-    hipLaunchKernelGGL((roi_pool_fwd_key_kernel<kKeyNT, CG, FX, HEAD>), grid, dim3(kKeyNT), pl.lds, st, x, rois, \
-                       static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd)
-    if (pl.cg == 16) {
-        if (fix7) FRCNN_KEY(16, 7); else FRCNN_KEY(16, 0);
-    } else if (pl.cg == 8) {
-        if (fix7) FRCNN_KEY(8, 7); else FRCNN_KEY(8, 0);
-    } else {
-        if (fix7) FRCNN_KEY(4, 7); else FRCNN_KEY(4, 0);
-    }
-#undef FRCNN_KEY
-    FRCNN_LAUNCH_CHECK("roi_pool_fwd_key_kernel");
-    return FRCNN_OK;
-}
-
-// Launch plan of the pair-tile forward: CG = 8 channel planes when the raw +
-// pair tiles (+ flags) fit the CU's LDS with room for a RoI-geometry chunk,
-// else 4; split as the wave kernel (one grid slot per resident workgroup of
-// the launch stream's CUs).  CG = 0: does not fit (the wave kernel runs).
-PxPlan pair_plan(int C, int N, int H, int W, int PHW, hipStream_t st) {
-    PxPlan pl;
-    const size_t HW = static_cast<size_t>(H) * W;
-    if (N <= 0 || HW == 0 || PHW > 64 || W > 255 || HW + 16 > (1 << 22)) return pl;  // flag word: w in 8 bits
-    constexpr size_t kReserve = 256;  // static LDS (s_red, s_next) + allocation rounding
-    constexpr size_t kPerGeo = sizeof(int4) + sizeof(int);
-    constexpr size_t kMinGeo = 64 * kPerGeo;
-    const size_t HWs = static_cast<size_t>(pair_hws(static_cast<int>(HW)));
-    for (int cg : {8, 4}) {
-        if (C % cg != 0) continue;
-        if (path_cfg().roi_cg && cg != path_cfg().roi_cg) continue;  // A/B override
-        const size_t tile = 2 * static_cast<size_t>(cg / 4) * HWs * sizeof(float4) + HWs * sizeof(uint16_t);
-        int per_cu = 0;
-        if (2 * (tile + kMinGeo + kReserve) <= kLdsPerCu) per_cu = 2;
-        else if (tile + kMinGeo + kReserve <= kLdsPerCu) per_cu = 1;
-        if (!per_cu) continue;
-        const size_t geo = (kLdsPerCu / per_cu - kReserve - tile) / kPerGeo;
-        pl.geo_cap = static_cast<int>(geo > 512 ? 512 : geo);
-        pl.cg = cg;
-        pl.lds = tile + static_cast<size_t>(pl.geo_cap) * kPerGeo;
-        const int64_t wgs = static_cast<int64_t>(C / cg) * N;
-        const int64_t slots = static_cast<int64_t>(stream_cu_count(st)) * per_cu;
-        // measured: the pair tiles win only with 8 channels per workgroup and
-        // one round of workgroups (cfg2); 4 channels (cfg4) or a second round
-        // (cfg5: 512 workgroups of one per CU) lose to the wave kernel
-        if (path_cfg().roi_fwd != kPathPair && (cg != 8 || wgs > slots)) return PxPlan{};
-        int64_t sp = (slots + wgs - 1) / wgs;
-        if (path_cfg().roi_split > 0) sp = path_cfg().roi_split;  // A/B override
-        pl.split = static_cast<int>(sp < 1 ? 1 : (sp > 64 ? 64 : sp));
-        return pl;
-    }
-    return pl;
-}
-
-template <bool HEAD>
-int pair_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
-                int PH, int PW, float ss, float* out, int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
-    const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(pl.split), static_cast<unsigned>(N + 1));
-    const bool fix7 = PH == 7 && PW == 7;
-#define FRCNN_PR(CG, FX)                                                                                     \
-    hipLaunchKernelGGL((roi_pool_fwd_pair_kernel<1024, CG, FX, HEAD>), grid, dim3(1024), pl.lds, st, x, rois, \
-                       static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd)
-    if (pl.cg == 8) {
-        if (fix7) FRCNN_PR(8, 7); else FRCNN_PR(8, 0);
-    } else {
-        if (fix7) FRCNN_PR(4, 7); else FRCNN_PR(4, 0);
-    }
-#undef FRCNN_PR
-    FRCNN_LAUNCH_CHECK("roi_pool_fwd_pair_kernel");
-    return FRCNN_OK;
-}
-
 // Launch plan of the dense forward: CG = 16 channel planes when they fit the
 // CU's LDS with room for a RoI chunk, else 8, else 4 (two workgroups per CU
 // when two fit); cap = RoIs per geometry chunk from the LDS left over; split =
@@ -2369,7 +1686,7 @@ int dense_launch(const DensePlan& pl, const float* x, const float* rois, const i
 }
 // One launch-plan choice for frcnn_roi_pool_fwd, frcnn_roi_pool_fwd_head and
 // the kernel-name query, so the name a caller records is the kernel launched.
-enum FwdKind { kFwdPair, kFwdKey, kFwdWave, kFwdDense, kFwdDenseList, kFwdGeneric };
+enum FwdKind { kFwdWave, kFwdDense, kFwdDenseList, kFwdGeneric };
 struct FwdChoice {
     int kind = kFwdGeneric;
     PxPlan px;
@@ -2380,17 +1697,7 @@ FwdChoice choose_fwd(int N, int C, int H, int W, int PH, int PW, bool sorted, hi
     const int path = path_cfg().roi_fwd;
     const int PHW = PH * PW;
     if (sorted && C > 0) {
-        // the pair-tile kernel only on request: alone it matched the wave kernel,
-        // beside other steps' kernels it lost (profiles/r3_experiments.md)
-        if (path == kPathPair && (ch.px = pair_plan(C, N, H, W, PHW, st)).cg) {
-            ch.kind = kFwdPair;
-            return ch;
-        }
-        if (path == kPathKey && (ch.px = key_plan(C, N, H, W, PHW, st)).cg) {
-            ch.kind = kFwdKey;
-            return ch;
-        }
-        if ((path == kPathAuto || path == kPathWave || path == kPathPair || path == kPathKey) &&
+        if ((path == kPathAuto || path == kPathWave) &&
             (ch.px = px_plan(C, N, H, W, PHW, st)).cg) {
             ch.kind = kFwdWave;
             return ch;
@@ -2409,8 +1716,6 @@ template <bool HEAD>
 int fwd_tile_launch(const FwdChoice& ch, const float* x, const float* rois, int64_t R, int N, int C, int H, int W,
                     int PH, int PW, float ss, float* out, int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
     switch (ch.kind) {
-        case kFwdPair: return pair_launch<HEAD>(ch.px, x, rois, R, N, C, H, W, PH, PW, ss, out, argmax, hd, st);
-        case kFwdKey: return key_launch<HEAD>(ch.px, x, rois, R, N, C, H, W, PH, PW, ss, out, argmax, hd, st);
         case kFwdWave: return px_launch<HEAD>(ch.px, x, rois, R, N, C, H, W, PH, PW, ss, out, argmax, hd, st);
         default:
             return dense_launch<HEAD, false>(ch.dn, x, rois, nullptr, nullptr, R, N, C, H, W, PH, PW, ss, out,
@@ -2482,8 +1787,6 @@ extern "C" int frcnn_roi_pool_fwd_kernel(int64_t R, int N, int C, int H, int W, 
     const char* hb = head == 1 ? "true" : "false";
     int n = 0;
     switch (ch.kind) {
-        case kFwdPair: n = snprintf(name, len, "roi_pool_fwd_pair_kernel<1024, %d, %d, %s>", ch.px.cg, fx, hb); break;
-        case kFwdKey: n = snprintf(name, len, "roi_pool_fwd_key_kernel<%d, %d, %d, %s>", kKeyNT, ch.px.cg, fx, hb); break;
         case kFwdWave:
             n = snprintf(name, len, "roi_pool_fwd_wave_kernel<1024, %d, %d, %s%s>", ch.px.cg, fx, hb,
                          path_cfg().roi_store ? ", true" : "");

@@ -291,22 +291,15 @@ __device__ unsigned long long g_samp_prof[16];
 #define SPROF_ADD(k, v) do {} while (0)
 #define SPROF_DT(k) do {} while (0)
 #endif
-#ifndef FRCNN_WIN_WAVES
-#define FRCNN_WIN_WAVES 12
-#endif
-constexpr int kWinWaves = FRCNN_WIN_WAVES;  // waves that walk a window; the others twist ahead
-#ifndef FRCNN_SAMP_SUBC
-#define FRCNN_SAMP_SUBC 1
-#endif
-constexpr int kSubc = FRCNN_SAMP_SUBC;     // 64-word chunks per walking wave and window
+// (windows of 2 / 4 chunks per wave measured 8 % / 32 % slower, 8 / 10 / 14 / 15 walking
+// waves and sequential thresholds of 256 / 512 / 2048 steps lost too: profiles/r4_experiments.md)
+constexpr int kWinWaves = 12;  // waves that walk a window; the others twist ahead
+constexpr int kSubc = 1;       // 64-word chunks per walking wave and window
 constexpr int kWinChunks = kWinWaves * kSubc;
 constexpr int kWin = kWinChunks * 64;      // words per window
 // a window (kWin words from pos <= 624) spans <= (624 + kWin - 1) / 624 + 1 blocks, + 1 being twisted
 constexpr int kRing = (kMtN + kWin - 1) / kMtN + 2;
-#ifndef FRCNN_SEQ_BELOW
-#define FRCNN_SEQ_BELOW 1024
-#endif
-constexpr int kSeqBelow = FRCNN_SEQ_BELOW;  // steps below which one wave walks the window
+constexpr int kSeqBelow = 1024;  // steps below which one wave walks the window
 static_assert(kSeqBelow <= (1 << 15), "the sequential walk's 16-bit fixed-point guess");
 
 struct Stream {  // block-uniform: every thread tracks the same values
@@ -1045,8 +1038,6 @@ __global__ __launch_bounds__(256) void bbox2reg_kernel(const TA* __restrict__ a,
     }
 }
 
-#include "draws.h"
-
 }  // namespace frcnn
 
 using namespace frcnn;
@@ -1070,26 +1061,8 @@ struct AtWs {
     int* sampled;
     int4* calls;  // [2N] per choice() call: cnt (0: none), lowest recorded step, p_hi, offset
     int* jrec;    // [2N][kMaxKeep] recorded swaps
-    DrawWs draw;  // the chip-wide draws (draws.h)
     size_t bytes;
 };
-// chip-wide draws of 2N calls of at most `steps` Fisher-Yates steps in all:
-// words for 2 * steps (every step accepts with probability >= 1/2) + 12 sigma
-void carve_draw(Carver& c, DrawWs& d, int N, double steps) {
-    const double words = 2.0 * steps + 12.0 * std::sqrt(2.0 * steps) + 1024.0;
-    d.chunks_max = static_cast<int>(words / kDrawChunk) + 2;
-    d.nblk_max = (kMtN + d.chunks_max * kDrawChunk) / kMtN + 2;
-    d.hdr = c.take<DrawHdr>(1);
-    d.c_ihi = c.take<int>(2 * N);
-    d.c_rlo = c.take<int>(2 * N);
-    d.c_slot = c.take<int>(2 * N);
-    d.c_u0 = c.take<int>(2 * N + 1);
-    d.seg = c.take<DrawSeg>(static_cast<size_t>(2 * N) * 24);
-    d.words = c.take<uint32_t>(static_cast<size_t>(d.nblk_max) * kMtN);
-    d.dir = c.take<uint4>(static_cast<size_t>(d.chunks_max) * kDrawEnt);
-    d.pool = c.take<uint32_t>(static_cast<size_t>(d.chunks_max) * kDrawEnt * 128);
-    d.sin = c.take<uint32_t>(d.chunks_max);
-}
 AtWs carve_at(void* ws, int N, int A, int Gp) {
     Carver c(ws);
     AtWs w{};
@@ -1110,29 +1083,11 @@ AtWs carve_at(void* ws, int N, int A, int Gp) {
     w.sampled = c.take<int>(2 * N);
     w.calls = c.take<int4>(2 * N);
     w.jrec = c.take<int>(static_cast<size_t>(2 * N) * kMaxKeep);
-    carve_draw(c, w.draw, N, static_cast<double>(N) * A);
     w.bytes = c.used();
     return w;
 }
 
-// the chip-wide draws (draws.h) on request: bit-exact, but slower than the
-// one-workgroup walk at the cfg5 shape (profiles/r4_experiments.md); the state
-// packs the call index in 10 bits
-bool use_chip_draws(int N) {
-    return path_cfg().sampler == kPathChip && 2 * N < kPlanMaxCalls;
-}
 
-int launch_draws(const DrawWs& d, uint32_t* rng, int* jrec, hipStream_t st) {
-    hipLaunchKernelGGL(draw_twist_kernel, dim3(1), dim3(256), 0, st, rng, d);
-    FRCNN_LAUNCH_CHECK("draw_twist_kernel");
-    hipLaunchKernelGGL(draw_chunk_kernel, dim3((d.chunks_max + 3) / 4), dim3(256), 0, st, d);
-    FRCNN_LAUNCH_CHECK("draw_chunk_kernel");
-    hipLaunchKernelGGL(draw_chain_kernel, dim3(1), dim3(kChainWaves * 64), 0, st, rng, d);
-    FRCNN_LAUNCH_CHECK("draw_chain_kernel");
-    hipLaunchKernelGGL(draw_replay_kernel, dim3((d.chunks_max + 255) / 256), dim3(256), 0, st, jrec, d);
-    FRCNN_LAUNCH_CHECK("draw_replay_kernel");
-    return FRCNN_OK;
-}
 }  // namespace
 
 #ifdef FRCNN_SAMPLER_PROF
@@ -1196,12 +1151,7 @@ extern "C" int frcnn_anchor_target_draw(int N, int A, int G, int n_sample, doubl
     FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_anchor_target_draw: workspace %zu < %zu",
                   ws_bytes, w.bytes);
     hipStream_t st = as_stream(stream);
-    if (rng_state && use_chip_draws(N)) {
-        hipLaunchKernelGGL(draw_plan_at_kernel, dim3(1), dim3(kPlanThreads), 0, st, N, n_sample, n_pos_max, w.npos, w.nneg,
-                           rng_state, w.sampled, w.calls, w.draw);
-        FRCNN_LAUNCH_CHECK("draw_plan_at_kernel");
-        return launch_draws(w.draw, rng_state, w.jrec, st);
-    } else if (rng_state) {
+    if (rng_state) {
         hipLaunchKernelGGL(at_sample_kernel, dim3(1), dim3(kSampThreads), 0, st, N, A, n_sample, n_pos_max,
                            w.pos_list, w.neg_list, w.npos, w.nneg, rng_state, w.sampled, w.calls, w.jrec);
         FRCNN_LAUNCH_CHECK("at_sample_kernel");
@@ -1280,7 +1230,6 @@ struct PtWs {
     int* spos;
     int4* calls;
     int* jrec;
-    DrawWs draw;
     size_t bytes;
 };
 PtWs carve_pt(void* ws, int N, int Rp, int Gp, int n_sample) {
@@ -1300,7 +1249,6 @@ PtWs carve_pt(void* ws, int N, int Rp, int Gp, int n_sample) {
     w.spos = c.take<int>(N);
     w.calls = c.take<int4>(2 * N);
     w.jrec = c.take<int>(static_cast<size_t>(2 * N) * kMaxKeep);
-    carve_draw(c, w.draw, N, static_cast<double>(N) * stride);
     w.bytes = c.used();
     return w;
 }
@@ -1355,12 +1303,6 @@ extern "C" int frcnn_proposal_target_draw(int N, int Rp, int G, int n_sample, do
     hipStream_t st = as_stream(stream);
     const int stride = Rp + Gp;
     const int pos_per_image = static_cast<int>(std::nearbyint(n_sample * pos_ratio));  // np.round
-    if (use_chip_draws(N)) {
-        hipLaunchKernelGGL(draw_plan_pt_kernel, dim3(1), dim3(kPlanThreads), 0, st, N, n_sample, pos_per_image, w.npos,
-                           w.nneg, rng_state, sample_count, w.spos, w.calls, w.draw);
-        FRCNN_LAUNCH_CHECK("draw_plan_pt_kernel");
-        return launch_draws(w.draw, rng_state, w.jrec, st);
-    }
     hipLaunchKernelGGL(pt_sample_kernel, dim3(1), dim3(kSampThreads), 0, st, N, stride, n_sample,
                        pos_per_image, w.pos_list, w.neg_list, w.npos, w.nneg, rng_state, sample_count, w.spos,
                        w.calls, w.jrec);
@@ -1481,12 +1423,4 @@ extern "C" int frcnn_bbox2reg(const void* anchors, int a_is_f64, const void* bbo
     return FRCNN_OK;
 }
 
-// The chip-wide draws' header of a workspace (tools/probe_draws.py): 12 ints +
-// 8 counters.  which = 0: anchor-target workspace (n = A), 1: proposal-target (n = Rp).
-extern "C" int frcnn_debug_draw_hdr(int which, int N, int n, int G, int n_sample, const void* workspace,
-                                    void* out) {
-    const int Gp = G > 0 ? G : 1;
-    const DrawHdr* h = which == 0 ? carve_at(const_cast<void*>(workspace), N, n, Gp).draw.hdr
-                                  : carve_pt(const_cast<void*>(workspace), N, n, Gp, n_sample).draw.hdr;
-    return hipMemcpy(out, h, sizeof(DrawHdr), hipMemcpyDeviceToHost) == hipSuccess ? 0 : FRCNN_EHIP;
-}
+

@@ -63,11 +63,11 @@ def test_set_path_accepts_the_documented_paths_only():
     accepted, anything else is rejected with rc=-1 and a message naming it."""
     from replication_faster_rcnn_amd import _lib
     lib = _lib.load(require_gpu=False)
-    ok = {"roi_pool_fwd": ["auto", "wave", "pair", "key", "dense", "generic"],
+    ok = {"roi_pool_fwd": ["auto", "wave", "dense", "generic"],
           "roi_pool_bwd": ["auto", "ring", "plain"],
           "propose": ["auto", "hybrid", "lazy", "wide"],
           "roi_pool_fwd_store": ["auto", "temporal", "nt"],
-          "sampler": ["auto", "walk", "chip"],
+          "sampler": ["auto", "walk"],
           "roi_pool_split": ["auto", "0", "7", "64"],
           "roi_pool_cg": ["auto", "4", "8", "16"]}
     try:
@@ -75,7 +75,8 @@ def test_set_path_accepts_the_documented_paths_only():
             for p in paths:
                 assert lib.frcnn_set_path(op.encode(), p.encode()) == 0, (op, p)
         for op, p in [("roi_pool_fwd_store", "streaming"), ("roi_pool_split", "65"), ("roi_pool_split", "x"),
-                      ("roi_pool_cg", "2"), ("sampler", "tiles"), ("no_such_op", "auto")]:
+                      ("roi_pool_cg", "2"), ("sampler", "tiles"), ("sampler", "chip"), ("roi_pool_fwd", "key"),
+                      ("roi_pool_fwd", "pair"), ("no_such_op", "auto")]:
             assert lib.frcnn_set_path(op.encode(), p.encode()) == -1, (op, p)
             assert p.encode() in lib.frcnn_last_error()
     finally:

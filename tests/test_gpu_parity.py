@@ -249,7 +249,7 @@ def test_propose_edge_cases(case, path):
 
 
 # forward paths: (kernel path, RoIs promised grouped by image)
-FWD_PATHS = [("key", True), ("wave", True), ("pair", True), ("dense", True), ("dense", False), ("generic", False)]
+FWD_PATHS = [("wave", True), ("dense", True), ("dense", False), ("generic", False)]
 
 
 def _special_x(r, N=2, C=16, H=12, W=14):
@@ -328,45 +328,13 @@ def test_roi_pool_paths_random(fpath, sorted_):
     assert np.array_equal(out.cpu().numpy(), oo)
 
 
-@pytest.mark.parametrize("case", ["one_class", "two_classes", "signed_zeros", "ties", "relu"])
-def test_roi_pool_key_class_collisions(case):
-    """The ordered-key forward's check: values that share a key class (equal
-    above the low 10 key bits) make the first pixel of the maximum's class
-    differ from the first maximum, which the kernel must detect and re-scan
-    exactly -- plateaus of one class, two interleaved classes, -0.0 / +0.0 in
-    either order (one class: -0.0 before +0.0 fails the check), exact
-    duplicates, ReLU-like zero windows; bit-exact vs the oracle."""
-    r = np.random.default_rng(sum(map(ord, case)))
-    N, C, H, W, R = 2, 16, 24, 40, 400
-    one = np.float32(1.0).view(np.uint32)
-    if case == "one_class":        # 1 + k ulp, k < 1024: every window is one class
-        x = (one + r.integers(0, 1000, (N, C, H, W))).astype(np.uint32).view(np.float32)
-    elif case == "two_classes":
-        x = (one + r.integers(0, 2048, (N, C, H, W))).astype(np.uint32).view(np.float32)
-    elif case == "signed_zeros":   # +0, -0, a negative, the smallest denormal (same class as the zeros)
-        v = np.array([0.0, -0.0, -1.0, 1e-45], np.float32)
-        x = v[r.choice(4, (N, C, H, W), p=[0.4, 0.4, 0.15, 0.05])]
-    elif case == "ties":
-        x = np.round(r.standard_normal((N, C, H, W)) * 2).astype(np.float32) / 2
-    else:
-        x = np.maximum(r.standard_normal((N, C, H, W)).astype(np.float32) - 0.8, 0).astype(np.float32)
-    b = np.sort(r.integers(0, N, R))
-    rois = _rand_rois(r, b, H, W, span=30)
-    with _lib.kernel_path("roi_pool_fwd", "key"):
-        out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7,
-                                           rois_sorted=True)
-    oo, oa = orc.roi_pool_forward(x, rois, 7)
-    assert np.array_equal(am.cpu().numpy(), oa)
-    assert np.array_equal(out.cpu().numpy().view(np.uint32), oo.view(np.uint32))
-
-
 def _rand_rois(r, b, H, W, lo=-3, span=40):
     xy = r.uniform(lo, max(H, W) + 2, (len(b), 2)).astype(np.float32)
     wh = r.uniform(0, span, (len(b), 2)).astype(np.float32)
     return np.concatenate([np.asarray(b, np.float32)[:, None], xy, xy + wh], 1).astype(np.float32)
 
 
-@pytest.mark.parametrize("fpath", ["key", "wave", "pair", "dense"])
+@pytest.mark.parametrize("fpath", ["wave", "dense"])
 @pytest.mark.parametrize("split", ["auto", "1", "3", "64"])
 @pytest.mark.parametrize("case", ["many_images", "invalid_ends", "unsorted", "single_roi", "gaps",
                                   "one_image_tiny_rois", "uniform_sizes", "ph5", "ph8x8", "ph3x9",
@@ -686,17 +654,12 @@ def test_roi_pool_bwd_poisoned_workspace(path):
 
 def test_roi_pool_fwd_kernel_label():
     """frcnn_roi_pool_fwd_kernel names what frcnn_roi_pool_fwd(_head) launches:
-    the wave kernel by default for RoIs grouped by image, the ordered-key and
-    pair-tile kernels on request, the dense kernel for unsorted RoIs (bench.py's
-    roofline label)."""
+    the wave kernel by default for RoIs grouped by image, the dense kernel for
+    unsorted RoIs (bench.py's roofline label)."""
     R, N, C, H, W = 2400, 8, 256, 38, 63
     assert _lib.roi_pool_fwd_kernel(R, N, C, H, W) == "roi_pool_fwd_wave_kernel<1024, 16, 7, true>"
     assert _lib.roi_pool_fwd_kernel(R, N, C, H, W, head=False) == "roi_pool_fwd_wave_kernel<1024, 16, 7, false>"
     assert _lib.roi_pool_fwd_kernel(2000, 1, 512, 50, 84) == "roi_pool_fwd_wave_kernel<1024, 8, 7, true>"
-    with _lib.kernel_path("roi_pool_fwd", "key"):
-        assert _lib.roi_pool_fwd_kernel(R, N, C, H, W) == "roi_pool_fwd_key_kernel<1024, 16, 7, true>"
-    with _lib.kernel_path("roi_pool_fwd", "pair"):
-        assert _lib.roi_pool_fwd_kernel(R, N, C, H, W) == "roi_pool_fwd_pair_kernel<1024, 8, 7, true>"
     assert _lib.roi_pool_fwd_kernel(R, N, C, H, W, rois_sorted=False, head=False).startswith(
         "roi_pool_fwd_dense_kernel<1024, 16, 7, false, true>")
     # the backward's label follows its plan (leader kernel for 7-wide bins, ring / plain on request)

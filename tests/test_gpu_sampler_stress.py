@@ -15,16 +15,6 @@ from replication_faster_rcnn_amd import synth, targets
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["walk", "chip"])
-def sampler_path(request):
-    """Every test on both samplers: the one-workgroup walk (default) and the
-    chip-wide chunk functions (draws.h, opt-in)."""
-    from replication_faster_rcnn_amd import _lib
-    _lib.set_path("sampler", request.param)
-    yield request.param
-    _lib.set_path("sampler", "auto")
-
-
 def _set_pos(seed, pos):
     """numpy's global state = the key after seed(seed), read position `pos` (0..624)."""
     np.random.seed(seed)

@@ -16,16 +16,6 @@ from replication_faster_rcnn_amd import synth, targets
 from replication_faster_rcnn_amd import utils as U
 
 
-@pytest.fixture(autouse=True, params=["walk", "chip"])
-def sampler_path(request):
-    """Every test on both samplers: the one-workgroup walk (default) and the
-    chip-wide chunk functions (draws.h, opt-in)."""
-    from replication_faster_rcnn_amd import _lib
-    _lib.set_path("sampler", request.param)
-    yield request.param
-    _lib.set_path("sampler", "auto")
-
-
 pytestmark = pytest.mark.gpu
 
 
