@@ -552,15 +552,36 @@ __device__ unsigned int g_pool_prof_rois[kPoolProfSlots];
 #define PPROF_ROIS(n) do {} while (0)
 #endif
 
-// Tile layout of the wave-per-RoI forward: 16-pixel groups, the group's NP
-// 4-channel planes back to back (pixel p of plane q at float4
-// (g*NP + q)*16 + s, g = p >> 4), the slot s = (p ^ g) & 15 XOR-swizzled so
-// that a ds_read_b128 of bins a bin width apart does not collide, and the
-// planes of one pixel 256 B apart -- LDS immediate offsets.
-template <int NP>
-__device__ __forceinline__ const float4* tile_px(const float4* q4, int p) {
-    const int g = p >> 4;
-    return q4 + g * (NP * 16) + ((p ^ g) & 15);
+// Tile layout of the wave-per-RoI forward: NP 4-channel planes, plane q at
+// byte q * PS, pixel p of a plane at byte 16 p (the tile starts at LDS address
+// 0: the kernel has no static LDS).  PS is a multiple of 256 B, so lanes
+// reading pixels p, p' collide only for p = p' mod 16 (a host-side model over
+// the bench's RoIs: 1.78 LDS passes per b128 read vs 1.89 for the XOR-swizzled
+// 16-pixel groups this replaced).  With PS a compile-time constant (KPS, the
+// 7x7 head on maps of < kFixPx pixels) a pixel's NP reads take two addresses
+// and immediate offsets, and the window walk steps one byte address: 3 VALU
+// per pixel besides the 3 per channel, against 8 for the swizzled layout.
+constexpr int kFixPx = 2432;  // pixels per plane (+ sentinel) at KPS = 38,912 B
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const f32x4 lds_f32x4;
+
+// Pixel reads at LDS byte address a (planes 0, 1 from a, planes 2, 3 from a2 =
+// a + 2 PS).  With a compile-time PS, a2 comes from an opaque add, else the
+// compiler re-derives a + 2 PS and a + 3 PS from a (two adds instead of one).
+template <int NP, int KPS>
+__device__ __forceinline__ void tile_read(uint32_t a, uint32_t ps, f32x4 (&v)[NP]) {
+    const uint32_t P = KPS ? static_cast<uint32_t>(KPS) : ps;
+    uint32_t a2 = 0;
+    if (NP > 2) {
+        if (KPS) asm("v_add_u32_e32 %0, %1, %2" : "=v"(a2) : "i"(2 * KPS), "v"(a));
+        else a2 = a + 2 * P;
+    }
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+        const uint32_t o = q < 2 ? a + q * P : a2 + (q - 2) * P;
+        v[q] = *reinterpret_cast<lds_f32x4*>(static_cast<size_t>(o));
+    }
 }
 
 // ------------------------------------------------- wave-per-RoI forward
@@ -585,20 +606,26 @@ __device__ __forceinline__ const float4* tile_px(const float4* q4, int p) {
 // shape per image or per RoI block -- are slower: DESIGN.md §3.)
 // FIX = PH = PW known at compile time (the 7x7 head): the 2 x CG output
 // stores of a RoI take immediate offsets from one base address.
-template <int NT, int CG, int FIX, bool HEAD, bool NTS = false>
+template <int NT, int CG, int FIX, bool HEAD, bool NTS = false, int KPS = 0>
 __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
     const float* __restrict__ x, const float* __restrict__ rois, int R, int C, int H, int W, int PH_, int PW_,
     float ss, float* __restrict__ out, int32_t* __restrict__ argmax, int geo_cap, HeadArgs hd) {
     const int PH = FIX ? FIX : PH_, PW = FIX ? FIX : PW_;
     constexpr int NP = CG / 4;
-    extern __shared__ __attribute__((aligned(16))) float4 q4[];  // plane k at q4 + k * HWs; geometry after
-    __shared__ int s_red[2 * (NT / 64)];
-    __shared__ int s_next;
+    // tile (NP planes of PS bytes, from address 0), geometry chunk, reduction
+    // scratch, work counter: all dynamic (no static LDS, so the tile is at 0)
+    extern __shared__ __attribute__((aligned(16))) float4 q4[];
+    char* const t = reinterpret_cast<char*>(q4);
+    if ((size_t)(__attribute__((address_space(3))) float4*)q4 != 0) __builtin_trap();  // the argmax decode needs it
     const int b = blockIdx.z;
     const int c0 = blockIdx.x * CG;
     const int tid = threadIdx.x, lane = tid & 63;
     const int HW = H * W;
     const int HWs = (HW + 16) & ~15;  // + the zero sentinel pixel HW
+    const uint32_t PS = KPS ? static_cast<uint32_t>(KPS) : static_cast<uint32_t>(HWs) * 16u;
+    int4* s_geo = reinterpret_cast<int4*>(t + NP * PS);
+    int* s_red = reinterpret_cast<int*>(s_geo + geo_cap);
+    int* s_next = s_red + 2 * (NT / 64);
     const int PHW = PH * PW;
     const int split = gridDim.y, z = blockIdx.y;
     const int N = gridDim.z - 1;
@@ -635,20 +662,21 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
     const int nmine = (nr - z + split - 1) / split;  // items z, z+split, ...
     PPROF_ROIS(nmine);
     const float* src = x + (static_cast<size_t>(b) * C + c0) * HW;
-    if (tid < NP) const_cast<float4*>(tile_px<NP>(q4, HW))[16 * tid] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < NP) *reinterpret_cast<float4*>(t + tid * PS + HW * 16) = make_float4(0.f, 0.f, 0.f, 0.f);
+    // Staged as max(v, -FLT_MAX) with NaN -> -FLT_MAX: no such value passes the
+    // scan's strict '>' against a running maximum >= -FLT_MAX, and the window's
+    // first pixel then starts the maximum as is (torchvision starts at -FLT_MAX).
     for (int p = tid; p < HW; p += NT) {
         float v[CG];
 #pragma unroll
         for (int q = 0; q < CG; ++q) {
             const float e = src[static_cast<size_t>(q) * HW + p];
-            v[q] = e;
+            v[q] = e > -FLT_MAX ? e : -FLT_MAX;
         }
-        const float4* pp = tile_px<NP>(q4, p);
 #pragma unroll
         for (int k = 0; k < NP; ++k)
-            const_cast<float4*>(pp)[16 * k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+            *reinterpret_cast<float4*>(t + k * PS + p * 16) = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
     }
-    int4* s_geo = reinterpret_cast<int4*>(q4 + NP * HWs);
     const int ph = lane / PW, pw = lane - (lane / PW) * PW;
     const bool act = lane < PHW;
     for (int k0 = 0; k0 < nmine; k0 += geo_cap) {
@@ -669,15 +697,15 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
             const RoiGeom gm = roi_geom(bx, ss, PH, PW);
             s_geo[i] = make_int4(gm.sh, gm.sw, __float_as_int(gm.bh), __float_as_int(gm.bw));
         }
-        if (tid == 0) s_next = 0;
+        if (tid == 0) *s_next = 0;
         __syncthreads();
         if (k0 == 0) PPROF_T(2);
         int k = 0;
-        if (lane == 0) k = atomicAdd(&s_next, 1);
+        if (lane == 0) k = atomicAdd(s_next, 1);
         k = __builtin_amdgcn_readfirstlane(k);
         while (k < cn) {
             int kn = 0;
-            if (lane == 0) kn = atomicAdd(&s_next, 1);  // prefetch the next item
+            if (lane == 0) kn = atomicAdd(s_next, 1);  // prefetch the next item
             const int r = rbase + z + (k0 + k) * split;
             const int4 gq = s_geo[k];
             RoiGeom gm;
@@ -688,37 +716,34 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
             int4 g = geom_bin(gm, H, W, ph, pw);
             if (!act) g = make_int4(0, 0, 0, 0);
             const bool empty = g.y <= g.x || g.w <= g.z;
-            // the window's first pixel starts the scan (torchvision's strict '>'
-            // against -FLT_MAX, no per-channel initialisation); an empty window
-            // reads the zero sentinel pixel and keeps argmax -1
+            // the window's first pixel starts the scan; an empty window reads the
+            // zero sentinel pixel and keeps argmax -1.  The argmax is carried as
+            // the pixel's byte address (16 p) and converted at the store.
             float mv[CG];
             int mi[CG];
             {
-                const int p0 = empty ? HW : g.x * W + g.z;
-                const float4* pp = tile_px<NP>(q4, p0);
-                float4 v[NP];
-#pragma unroll
-                for (int q = 0; q < NP; ++q) v[q] = pp[16 * q];
+                const uint32_t a0 = static_cast<uint32_t>(empty ? HW : g.x * W + g.z) * 16u;
+                const float thr = empty ? __int_as_float(0x7f800000) : -FLT_MAX;
+                f32x4 v[NP];
+                tile_read<NP, KPS>(a0, PS, v);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int q = 0; q < NP; ++q) {
                     const float vv[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
-                        const bool gt = vv[j] > -FLT_MAX;
-                        mv[4 * q + j] = gt ? vv[j] : -FLT_MAX;
-                        mi[4 * q + j] = (gt && !empty) ? p0 : -1;
+                        mv[4 * q + j] = vv[j];
+                        mi[4 * q + j] = vv[j] > thr ? static_cast<int>(a0) : -1;
                     }
                 }
             }
             for (int h = g.x; h < g.y; ++h) {
-                const int rb = h * W;
-                for (int w = h == g.x ? g.z + 1 : g.z; w < g.w; ++w) {
-                    const int ii = rb + w;
-                    const float4* pp = tile_px<NP>(q4, ii);
-                    float4 v[NP];
-#pragma unroll
-                    for (int q = 0; q < NP; ++q) v[q] = pp[16 * q];
+                const uint32_t rb = static_cast<uint32_t>(h * W) * 16u;
+                const uint32_t ae = rb + static_cast<uint32_t>(g.w) * 16u;
+                uint32_t a = rb + static_cast<uint32_t>(h == g.x ? g.z + 1 : g.z) * 16u;
+                for (; a < ae; a += 16) {
+                    f32x4 v[NP];
+                    tile_read<NP, KPS>(a, PS, v);
                     // all NP reads in flight before the first compare (else the compiler
                     // waits on each read in turn: NP LDS round trips per pixel)
                     __builtin_amdgcn_sched_barrier(0);
@@ -729,7 +754,7 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
                         for (int j = 0; j < 4; ++j) {
                             if (vv[j] > mv[4 * q + j]) {  // torchvision's strict '>'
                                 mv[4 * q + j] = vv[j];
-                                mi[4 * q + j] = ii;
+                                mi[4 * q + j] = static_cast<int>(a);
                             }
                         }
                     }
@@ -749,13 +774,13 @@ __global__ __launch_bounds__(NT) void roi_pool_fwd_wave_kernel(
 #pragma unroll
                     for (int c = 0; c < CG; ++c) {
                         __builtin_nontemporal_store(mv[c], op + c * PHW);
-                        __builtin_nontemporal_store(mi[c], ap + c * PHW);
+                        __builtin_nontemporal_store(mi[c] >> 4, ap + c * PHW);
                     }
                 } else {
 #pragma unroll
                     for (int c = 0; c < CG; ++c) {
                         op[c * PHW] = mv[c];
-                        ap[c * PHW] = mi[c];
+                        ap[c * PHW] = mi[c] >> 4;
                     }
                 }
             }
@@ -1568,27 +1593,31 @@ FwdWs carve_fwd(void* ws, int64_t R, int N) {
 // resident slot of the CUs the launch stream may use once.
 struct PxPlan {
     int cg = 0, geo_cap = 0, split = 1;
+    bool kps = false;  // plane stride = kFixPx pixels (compile time)
     size_t lds = 0;
 };
+constexpr size_t kWaveScratch = 256;  // the wave kernel's reduction scratch + work counter
 PxPlan px_plan(int C, int N, int H, int W, int PHW, hipStream_t st, size_t per_geo = sizeof(int4)) {
     PxPlan pl;
     const size_t HW = static_cast<size_t>(H) * W;
     if (N <= 0 || HW == 0 || PHW > 64 || H > 65535 || W > 65535) return pl;
-    constexpr size_t kReserve = 1024;  // static LDS + allocation rounding
+    constexpr size_t kReserve = 1024;  // allocation rounding
     const size_t kMinGeo = 64 * per_geo;
     const size_t HWs = (HW + 16) & ~static_cast<size_t>(15);  // + the zero sentinel pixel
     for (int cg : {16, 8, 4}) {
         if (C % cg != 0) continue;
         if (path_cfg().roi_cg && cg != path_cfg().roi_cg) continue;  // A/B override
-        const size_t tile = static_cast<size_t>(cg / 4) * HWs * sizeof(float4);
+        const bool kps = cg == 16 && PHW == 49 && HWs <= static_cast<size_t>(kFixPx);
+        const size_t tile = static_cast<size_t>(cg / 4) * (kps ? kFixPx : HWs) * sizeof(float4);
         int per_cu = 0;
-        if (2 * (tile + kMinGeo + kReserve) <= kLdsPerCu) per_cu = 2;
-        else if (tile + kMinGeo + kReserve <= kLdsPerCu) per_cu = 1;
+        if (2 * (tile + kMinGeo + kWaveScratch + kReserve) <= kLdsPerCu) per_cu = 2;
+        else if (tile + kMinGeo + kWaveScratch + kReserve <= kLdsPerCu) per_cu = 1;
         if (!per_cu) continue;
-        const size_t geo = (kLdsPerCu / per_cu - kReserve - tile) / per_geo;
+        const size_t geo = (kLdsPerCu / per_cu - kReserve - kWaveScratch - tile) / per_geo;
         pl.geo_cap = static_cast<int>(geo > 512 ? 512 : geo);
         pl.cg = cg;
-        pl.lds = tile + static_cast<size_t>(pl.geo_cap) * per_geo;
+        pl.kps = kps;
+        pl.lds = tile + static_cast<size_t>(pl.geo_cap) * per_geo + kWaveScratch;
         const int64_t wgs = static_cast<int64_t>(C / cg) * N;
         int64_t sp = (static_cast<int64_t>(stream_cu_count(st)) * per_cu + wgs - 1) / wgs;
         if (path_cfg().roi_split > 0) sp = path_cfg().roi_split;  // A/B override
@@ -1603,21 +1632,23 @@ int px_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, in
               int PH, int PW, float ss, float* out, int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
     const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(pl.split), static_cast<unsigned>(N + 1));
     const bool fix7 = PH == 7 && PW == 7;
-#define FRCNN_PX(CG, FX)                                                                                         \
+#define FRCNN_PX(CG, FX, KP)                                                                                    \
     do {                                                                                                         \
         if (path_cfg().roi_store)                                                                                \
-            hipLaunchKernelGGL((roi_pool_fwd_wave_kernel<1024, CG, FX, HEAD, true>), grid, dim3(1024), pl.lds, st, \
-                               x, rois, static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd);  \
+            hipLaunchKernelGGL((roi_pool_fwd_wave_kernel<1024, CG, FX, HEAD, true, KP>), grid, dim3(1024), pl.lds, \
+                               st, x, rois, static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd); \
         else                                                                                                     \
-            hipLaunchKernelGGL((roi_pool_fwd_wave_kernel<1024, CG, FX, HEAD>), grid, dim3(1024), pl.lds, st, x,    \
-                               rois, static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd);    \
+            hipLaunchKernelGGL((roi_pool_fwd_wave_kernel<1024, CG, FX, HEAD, false, KP>), grid, dim3(1024), pl.lds, \
+                               st, x, rois, static_cast<int>(R), C, H, W, PH, PW, ss, out, argmax, pl.geo_cap, hd); \
     } while (0)
     if (pl.cg == 16) {
-        if (fix7) FRCNN_PX(16, 7); else FRCNN_PX(16, 0);
+        if (pl.kps) FRCNN_PX(16, 7, kFixPx * 16);
+        else if (fix7) FRCNN_PX(16, 7, 0);
+        else FRCNN_PX(16, 0, 0);
     } else if (pl.cg == 8) {
-        if (fix7) FRCNN_PX(8, 7); else FRCNN_PX(8, 0);
+        if (fix7) FRCNN_PX(8, 7, 0); else FRCNN_PX(8, 0, 0);
     } else {
-        if (fix7) FRCNN_PX(4, 7); else FRCNN_PX(4, 0);
+        if (fix7) FRCNN_PX(4, 7, 0); else FRCNN_PX(4, 0, 0);
     }
 #undef FRCNN_PX
     FRCNN_LAUNCH_CHECK("roi_pool_fwd_wave_kernel");
@@ -1788,8 +1819,12 @@ extern "C" int frcnn_roi_pool_fwd_kernel(int64_t R, int N, int C, int H, int W, 
     int n = 0;
     switch (ch.kind) {
         case kFwdWave:
-            n = snprintf(name, len, "roi_pool_fwd_wave_kernel<1024, %d, %d, %s%s>", ch.px.cg, fx, hb,
-                         path_cfg().roi_store ? ", true" : "");
+            if (ch.px.kps)
+                n = snprintf(name, len, "roi_pool_fwd_wave_kernel<1024, %d, %d, %s, %s, %d>", ch.px.cg, fx, hb,
+                             path_cfg().roi_store ? "true" : "false", kFixPx * 16);
+            else
+                n = snprintf(name, len, "roi_pool_fwd_wave_kernel<1024, %d, %d, %s%s>", ch.px.cg, fx, hb,
+                             path_cfg().roi_store ? ", true" : "");
             break;
         case kFwdDense:
             n = snprintf(name, len, "roi_pool_fwd_dense_kernel<1024, %d, %d, %s, false>", ch.dn.cg, fx, hb);
