@@ -87,12 +87,21 @@ __device__ __forceinline__ float box_area(float4 b) {
 
 constexpr uint64_t kInvalidKey = ~0ull;
 
+// The proposal chain's kernels (decode, first-chunk select / sort, IoU tiles,
+// sweep) raise their waves' issue priority: in the bench pipeline they share
+// CUs with the previous steps' RoIPool waves, which are VALU bound, and each
+// chain is a step stream's serial latency (chain, then its pool).  cfg2 driver
+// command 92.9-97.0k -> 100.1-101.2k images/s; cfg1 / cfg4 / cfg5 unchanged
+// (profiles/r5_experiments.md).
+#define FRCNN_CHAIN_PRIO() __builtin_amdgcn_s_setprio(3)
+
 // ---------------------------------------------------------------- 1. decode
 __global__ __launch_bounds__(256) void decode_filter_kernel(
     const float* __restrict__ scores, const float4* __restrict__ deltas,
     const float4* __restrict__ anchors, const float4* __restrict__ base, int A, int K, int W,
     int stride, float img_h, float img_w, float min_size, float4* __restrict__ boxes,
     uint64_t* __restrict__ keys) {
+    FRCNN_CHAIN_PRIO();
     int a = blockIdx.x * 256 + threadIdx.x;
     if (a >= A) return;
     size_t o = static_cast<size_t>(blockIdx.y) * A + a;
@@ -591,6 +600,7 @@ constexpr int kChunkBlocks = kChunk / 64;                           // 16
 __global__ __launch_bounds__(256) void chunk_colmask_kernel(const float4* __restrict__ cbox_all,
                                                             const int* __restrict__ cc_all, NmsThr thr,
                                                             uint64_t* __restrict__ colT, int nbt) {
+    FRCNN_CHAIN_PRIO();
     const int n = blockIdx.y;
     const int cc = cc_all[n];
     const int nb = (cc + 63) / 64;
@@ -709,6 +719,7 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
     const uint64_t* __restrict__ keys_all, const float4* __restrict__ boxes_all, int A, int pre,
     int post, NmsThr thr, float4* __restrict__ out_rois, int32_t* __restrict__ out_idx,
     int32_t* __restrict__ out_count, HybWs hw, int first) {
+    FRCNN_CHAIN_PRIO();
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     __shared__ FusedShared sh;
     unsigned* hist = reinterpret_cast<unsigned*>(lds_raw);                          // 16 KB
