@@ -561,7 +561,7 @@ __device__ unsigned int g_pool_prof_rois[kPoolProfSlots];
 // 7x7 head on maps of < kFixPx pixels) a pixel's NP reads take two addresses
 // and immediate offsets, and the window walk steps one byte address: 3 VALU
 // per pixel besides the 3 per channel, against 8 for the swizzled layout.
-constexpr int kFixPx = 2432;  // pixels per plane (+ sentinel) at KPS = 38,912 B
+constexpr int kFixPx = 2400;  // pixels per plane (+ sentinel) at KPS = 38,400 B (38 x 63 + 1 fits)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const f32x4 lds_f32x4;
@@ -1597,6 +1597,7 @@ struct PxPlan {
     size_t lds = 0;
 };
 constexpr size_t kWaveScratch = 256;  // the wave kernel's reduction scratch + work counter
+constexpr size_t kGeoCap = 368;       // RoIs per geometry chunk (see px_plan)
 PxPlan px_plan(int C, int N, int H, int W, int PHW, hipStream_t st, size_t per_geo = sizeof(int4)) {
     PxPlan pl;
     const size_t HW = static_cast<size_t>(H) * W;
@@ -1614,7 +1615,9 @@ PxPlan px_plan(int C, int N, int H, int W, int PHW, hipStream_t st, size_t per_g
         else if (tile + kMinGeo + kWaveScratch + kReserve <= kLdsPerCu) per_cu = 1;
         if (!per_cu) continue;
         const size_t geo = (kLdsPerCu / per_cu - kReserve - kWaveScratch - tile) / per_geo;
-        pl.geo_cap = static_cast<int>(geo > 512 ? 512 : geo);
+        // geometry chunk: at most kGeoCap RoIs, so that a 16-plane workgroup leaves
+        // 4 KB of the CU's LDS to the proposal chain's IoU-tile kernel (3.3 KB)
+        pl.geo_cap = static_cast<int>(geo > kGeoCap ? kGeoCap : geo);
         pl.cg = cg;
         pl.kps = kps;
         pl.lds = tile + static_cast<size_t>(pl.geo_cap) * per_geo + kWaveScratch;

@@ -301,7 +301,7 @@ def test_roi_pool_nontemporal_stores():
     with _lib.kernel_path("roi_pool_fwd", "wave"), _lib.kernel_path("roi_pool_fwd_store", "nt"):
         out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV), 7,
                                            rois_sorted=True)
-        assert _lib.roi_pool_fwd_kernel(len(rois), N, x.shape[1], x.shape[2], x.shape[3]).endswith(", true, 38912>")
+        assert _lib.roi_pool_fwd_kernel(len(rois), N, x.shape[1], x.shape[2], x.shape[3]).endswith(", true, 38400>")
     oo, oa = orc.roi_pool_forward(x, rois, 7)
     assert np.array_equal(am.cpu().numpy(), oa)
     assert np.array_equal(out.cpu().numpy().view(np.uint32), oo.view(np.uint32))
@@ -657,8 +657,8 @@ def test_roi_pool_fwd_kernel_label():
     the wave kernel by default for RoIs grouped by image, the dense kernel for
     unsorted RoIs (bench.py's roofline label)."""
     R, N, C, H, W = 2400, 8, 256, 38, 63
-    assert _lib.roi_pool_fwd_kernel(R, N, C, H, W) == "roi_pool_fwd_wave_kernel<1024, 16, 7, true, false, 38912>"
-    assert _lib.roi_pool_fwd_kernel(R, N, C, H, W, head=False) == "roi_pool_fwd_wave_kernel<1024, 16, 7, false, false, 38912>"
+    assert _lib.roi_pool_fwd_kernel(R, N, C, H, W) == "roi_pool_fwd_wave_kernel<1024, 16, 7, true, false, 38400>"
+    assert _lib.roi_pool_fwd_kernel(R, N, C, H, W, head=False) == "roi_pool_fwd_wave_kernel<1024, 16, 7, false, false, 38400>"
     assert _lib.roi_pool_fwd_kernel(2000, 1, 512, 50, 84) == "roi_pool_fwd_wave_kernel<1024, 8, 7, true>"
     assert _lib.roi_pool_fwd_kernel(R, N, C, H, W, rois_sorted=False, head=False).startswith(
         "roi_pool_fwd_dense_kernel<1024, 16, 7, false, true>")
