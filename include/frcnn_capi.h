@@ -53,8 +53,8 @@ int frcnn_probe_hw_ids(uint32_t* out, int nblocks, int spin, void* stream);
 
 /* Kernel-path selection, process-global (tests and A/B tools; the default
  * "auto" is what every caller should use).  op / path:
- *   "roi_pool_fwd"   : "auto" | "wave" (raw image tile in LDS, compare-and-select scan, one
- *                      wave per RoI; RoIs grouped by image; the auto choice) | "dense" (image
+ *   "roi_pool_fwd"   : "auto" | "wave" (plane-major image tile in LDS, compare-and-select scan,
+ *                      one wave per RoI; RoIs grouped by image; the auto choice) | "dense" (image
  *                      tile, bins packed 64 per wave; any RoI order) | "generic" (one
  *                      workgroup per RoI)
  *   "roi_pool_bwd"   : "auto" (leader-gather plane owner for 7-wide outputs, else ring) | "ring" (latency-hidden plane owner) | "plain"
@@ -178,7 +178,7 @@ int frcnn_roi_pool_fwd_head(const float* x, const float* rois, const float* roi_
  * an unaligned rois pointer, which the head entry point handles as transform +
  * the plain forward) or frcnn_roi_pool_fwd (head == 0) launches for this shape on
  * `stream` under the current frcnn_set_path choices, as its template name (e.g.
- * "roi_pool_fwd_pair_kernel<1024, 8, 7, true>"), NUL-terminated in name[len]:
+ * "roi_pool_fwd_wave_kernel<1024, 16, 7, true, false, 38400>"), NUL-terminated in name[len]:
  * the label bench.py and the rocprofv3 records key the dominant kernel on. */
 int frcnn_roi_pool_fwd_kernel(int64_t R, int N, int C, int H, int W, int PH, int PW, int rois_sorted,
                               int head, void* stream, char* name, size_t len);
