@@ -802,8 +802,11 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
         if (r_done == 0) PRPROF(3);
         // ---- sort of the chunk, ascending: every wave bitonic-sorts its 64 keys
         // with shuffles; a key's final position is its rank = the number of keys
-        // below it over the 16 sorted runs (binary searches; valid keys are
-        // distinct, the invalid padding sorts last and is not placed)
+        // below it over the chunk's sorted runs (binary searches; valid keys are
+        // distinct, the invalid padding sorts last and is not placed).  Only the
+        // nrun waves that hold keys search (the other runs are all padding).
+        const int nrun = (cc + 63) >> 6;
+        const bool inrun = wid < nrun;  // wave-uniform
         uint64_t key = tid < cc ? ckey[tid] : kInvalidKey;
         for (int kk = 2; kk <= 64; kk <<= 1) {
             for (int j = kk >> 1; j > 0; j >>= 1) {
@@ -819,19 +822,20 @@ __global__ __launch_bounds__(1024) void propose_fused_kernel(
         ckey[tid] = key;
         __syncthreads();
         int rank = lane;  // within its own run
+        if (inrun) {
+            for (int w = 0; w < nrun; ++w) {
+                if (w == wid) continue;
+                const uint64_t* run = ckey + w * 64;
+                int lo = 0;
 #pragma unroll
-        for (int w = 0; w < kChunk / 64; ++w) {
-            if (w == wid) continue;
-            const uint64_t* run = ckey + w * 64;
-            int lo = 0;
-#pragma unroll
-            for (int step = 32; step > 0; step >>= 1)
-                if (run[lo + step - 1] < key) lo += step;
-            lo += run[lo] < key ? 1 : 0;
-            rank += lo;
+                for (int step = 32; step > 0; step >>= 1)
+                    if (run[lo + step - 1] < key) lo += step;
+                lo += run[lo] < key ? 1 : 0;
+                rank += lo;
+            }
         }
         __syncthreads();
-        if (key != kInvalidKey) ckey[rank] = key;
+        if (inrun && key != kInvalidKey) ckey[rank] = key;
         __syncthreads();
         key = ckey[tid];
         ckey[tid] = key;
