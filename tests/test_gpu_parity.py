@@ -103,6 +103,33 @@ def test_propose_batched_full_size(golden, cfg, imgs, path):
         assert (idx[j, k:] == -1).all()
 
 
+def test_propose_continuation_vs_oracle(path):
+    """Scores peaked at the image centre: NMS suppresses most of the top candidates,
+    so the 300th kept box is candidate ~1,250 of 6,000 (asserted on the oracle) and
+    the hybrid path's sweep (first chunk 512 rows, from global scratch) must run
+    the lazy continuation over two more chunks.  Bit-exact vs the oracle."""
+    c = synth.CONFIGS["cfg2"]
+    anchors = orc.generate_anchors(orc.generate_anchor_base(), 16, c["feat_w"], c["feat_h"])
+    n = len(anchors)
+    r = np.random.default_rng(3)
+    cy = (anchors[:, 0] + anchors[:, 2]) / 2
+    cx = (anchors[:, 1] + anchors[:, 3]) / 2
+    scores = (np.exp(-((cy - 300) ** 2 + (cx - 500) ** 2) / 200.0 ** 2) + 0.01 * r.random(n)).astype(np.float32)
+    deltas = np.zeros((n, 4), np.float32)
+    bbox = orc.reg2bbox(anchors, deltas)
+    bbox[:, [0, 2]] = np.clip(bbox[:, [0, 2]], 0, c["img_h"])
+    bbox[:, [1, 3]] = np.clip(bbox[:, [1, 3]], 0, c["img_w"])
+    m = (bbox[:, 2] - bbox[:, 0] >= 16) & (bbox[:, 3] - bbox[:, 1] >= 16)
+    s = scores[np.nonzero(m)[0]]
+    rank = np.argsort(-s, kind="stable")[:c["pre_nms"]]
+    keep_all = orc.nms(bbox[np.nonzero(m)[0]][rank], s[rank], 0.7)
+    assert keep_all[c["post_nms"] - 1] >= 1024  # the continuation is exercised
+    rois, idx = _propose_one_gpu(anchors, scores, deltas, c["img_w"], c["img_h"], c["pre_nms"], c["post_nms"])
+    orois, oidx = orc.propose_one(anchors, scores, deltas, c["img_w"], c["img_h"], c["pre_nms"], c["post_nms"])
+    assert np.array_equal(idx, oidx)
+    assert np.array_equal(rois, orois)
+
+
 def test_propose_batch_invariance(path):
     """P-invariance: an image's proposals do not depend on its batch mates."""
     c = synth.CONFIGS["cfg2"]
