@@ -91,7 +91,8 @@ constexpr uint64_t kInvalidKey = ~0ull;
 // sweep) raise their waves' issue priority: in the bench pipeline they share
 // CUs with the previous steps' RoIPool waves, which are VALU bound, and each
 // chain is a step stream's serial latency (chain, then its pool).  cfg2 driver
-// command 92.9-97.0k -> 100.1-101.2k images/s; cfg1 / cfg4 / cfg5 unchanged
+// command 92.9-97.0k -> 100.1-101.2k images/s; the wide path's sort / NMS
+// kernels likewise: cfg1 10.9-11.0k -> 11.3k, cfg4 7.1k -> 7.2-7.3k
 // (profiles/r5_experiments.md).
 #define FRCNN_CHAIN_PRIO() __builtin_amdgcn_s_setprio(3)
 
@@ -166,6 +167,7 @@ __device__ __forceinline__ int lower_bound_u64(const uint64_t* s, int len, uint6
 
 __global__ __launch_bounds__(1024) void run_sort_kernel(const uint64_t* __restrict__ keys_all, int A, int nr,
                                                         uint64_t* __restrict__ runs_all, int* __restrict__ vcount) {
+    FRCNN_CHAIN_PRIO();
     const int n = blockIdx.y, i = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int base = i * kRun;
@@ -206,6 +208,7 @@ __global__ __launch_bounds__(1024) void run_sort_kernel(const uint64_t* __restri
 // Workgroup (i, j): for every key of run i, the number of keys of run j below it.
 __global__ __launch_bounds__(1024) void merge_rank_kernel(const uint64_t* __restrict__ runs_all, int A, int nr,
                                                           int* __restrict__ part) {
+    FRCNN_CHAIN_PRIO();
     const int n = blockIdx.z, j = blockIdx.y, i = blockIdx.x;
     if (i == j) return;
     const int tid = threadIdx.x;
@@ -234,6 +237,7 @@ __global__ __launch_bounds__(1024) void rank_scatter_kernel(const uint64_t* __re
                                                             int pre, const float4* __restrict__ box_src,
                                                             float4* __restrict__ sbox, int32_t* __restrict__ sidx,
                                                             int* __restrict__ sel_P, SweepState ss) {
+    FRCNN_CHAIN_PRIO();
     const int n = blockIdx.y, i = blockIdx.x;
     const int tid = threadIdx.x;
     int nvalid = 0;
@@ -307,6 +311,7 @@ __global__ __launch_bounds__(256) void nms_mask_stage_kernel(const float4* __res
                                                              uint64_t* __restrict__ maskC,
                                                              const uint64_t* __restrict__ kept_all,
                                                              uint64_t* __restrict__ prehit) {
+    FRCNN_CHAIN_PRIO();
     const int n = blockIdx.y;
     if (done[n]) return;
     const int P = sel_P[n];
@@ -385,6 +390,7 @@ __global__ __launch_bounds__(1024) void nms_sweep_stage_kernel(
     const int32_t* __restrict__ sidx_all, int pre, int Wc, const int* __restrict__ sel_P, int post,
     int cb0, int cb1, SweepState ss, float4* __restrict__ out_rois, int32_t* __restrict__ out_idx,
     int64_t* __restrict__ out_keep, int32_t* __restrict__ out_count) {
+    FRCNN_CHAIN_PRIO();
     extern __shared__ __attribute__((aligned(16))) uint64_t kept[];  // [Wc]
     __shared__ uint64_t s_K[2];
     __shared__ int s_count[2];
