@@ -406,6 +406,11 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     int i_cur = i_hi;
+    // S.rec's buffer parity runs on across windows: a wave reading the last round's
+    // counts of one window and a wave publishing the next window's first round use
+    // different buffers, so a window needs no closing barrier (its round barriers
+    // order the ring-word reads before the next twists)
+    int par = 0;
     while (i_cur >= 1) {
         const int need = (st.off + kWin - 1) / kMtN;  // blocks past st.slot this window reaches
         {
@@ -514,7 +519,7 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
         // the new prefix; the waves before it are settled.  Counts hardly depend on
         // the base, so the first round's guesses are usually inside the margins and
         // the rest settle in the second; each round settles at least one more wave.
-        int il[kSubc], total = 0, par = 0;
+        int il[kSubc], total = 0;
         uint32_t m[kSubc];
         bool a[kSubc];
 #pragma unroll
@@ -630,8 +635,8 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
             st.slot = (st.slot + 1) % kRing;
             --st.ngen;
         }
-        __syncthreads();  // this window's reads of S done before the next twist / counts
     }
+    __syncthreads();  // the call's swap records (J) and S.last are read next
 }
 
 // Final values at permutation positions [p_lo, p_hi) of the cnt-element
