@@ -473,14 +473,15 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
                     i_loc -= cntc;
                     SPROF_ADD(9, 1);
                 }
-                if (lane == 0) {
-                    S.last[0] = i_loc;
-                    S.last[1] = used;
+                if (lane == 0) {  // (double-buffered by the parity: no closing barrier)
+                    S.last[2 * (par & 1)] = i_loc;
+                    S.last[2 * (par & 1) + 1] = used;
                 }
             }
             __syncthreads();
             SPROF_DT(10);
-            const int i_new = S.last[0], consumed = S.last[1];
+            const int i_new = S.last[2 * (par & 1)], consumed = S.last[2 * (par & 1) + 1];
+            par ^= 1;
             i_cur = i_new;
             if (gen) ++st.ngen;
             st.off += consumed;
@@ -489,7 +490,6 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
                 st.slot = (st.slot + 1) % kRing;
                 --st.ngen;
             }
-            __syncthreads();
             continue;
         }
         // wave wid walks chunks wid * kSubc .. + kSubc - 1 (64 words each, in
