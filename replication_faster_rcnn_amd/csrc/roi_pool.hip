@@ -587,7 +587,7 @@ __device__ __forceinline__ void tile_read(uint32_t a, uint32_t ps, f32x4 (&v)[NP
 // ------------------------------------------------- wave-per-RoI forward
 // The default forward for RoIs grouped by image.  Grid (C/CG, split, N + 1):
 // one 1024-thread workgroup owns CG channel planes of one image (staged once
-// into LDS, tile_px layout) and a strided
+// into LDS as plane-major 4-channel planes, see tile_read) and a strided
 // share of that image's RoIs (items z, z+split, ...: RoI sizes are
 // uncorrelated with rank, so every share sees the image's size mix).  One
 // wave per RoI, lane = bin: each lane walks its window once and updates CG
@@ -602,8 +602,9 @@ __device__ __forceinline__ void tile_read(uint32_t a, uint32_t ps, f32x4 (&v)[NP
 // index is the slowest grid dimension, so the workgroups of row N (RoIs with a
 // batch index outside [0, N): usually none, they exit at once) are dispatched
 // after every real one instead of holding CUs between them.
-// (Measured alternatives -- RoI bins packed 64 per wave, bins sorted by window
-// shape per image or per RoI block -- are slower: DESIGN.md §3.)
+// (Measured alternatives -- RoI bins packed 64 per wave, bins or rows sorted by
+// window shape, RoIs in cost order, a byte window table -- are slower:
+// DESIGN.md §3, profiles/r5_experiments.md.)
 // FIX = PH = PW known at compile time (the 7x7 head): the 2 x CG output
 // stores of a RoI take immediate offsets from one base address.
 template <int NT, int CG, int FIX, bool HEAD, bool NTS = false, int KPS = 0>
