@@ -1268,7 +1268,10 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_pf_kernel(
 // load waits), in the neighbour exchanges, and applying to the plane.
 #ifdef FRCNN_BWD_PROF
 constexpr int kBwdProfWaves = 8192;
-__device__ unsigned long long g_bwd_prof[kBwdProfWaves][4];
+// columns: the three phases, the RoI count, then the wave's start and end on the
+// constant 100 MHz clock (s_memrealtime), the end after its plane write-out, then the
+// wave's flagged (ranked) RoIs
+__device__ unsigned long long g_bwd_prof[kBwdProfWaves][8];
 #define BPROF_T() __builtin_amdgcn_s_memtime()
 #else
 #define BPROF_T() 0ull
@@ -1308,6 +1311,9 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
     const int b = blockIdx.y;
     const int c = blockIdx.x * CPW + wid;
     if (c >= C) return;  // whole wave; no workgroup barrier below
+#ifdef FRCNN_BWD_PROF
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     float* gplane = grad_in + (static_cast<size_t>(b) * C + c) * HW;
     // HWs >= HW + 64: word HW + lane is lane's dummy (a word per lane, so the
     // non-leaders' writes do not serialise on one bank)
@@ -1371,7 +1377,7 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
             mask_load(e, cl_r[d], ch_r[d]);
             asm volatile("" ::: "memory");
         }
-        unsigned long long tp[3] = {0, 0, 0};
+        unsigned long long tp[4] = {0, 0, 0, 0};
         for (int t0 = 0; t0 < nr; t0 += D) {
             const unsigned long long p0 = BPROF_T();
             int nx[D];
@@ -1508,6 +1514,10 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
             tp[0] += p1 - p0;
             tp[1] += p2 - p1;
             tp[2] += p3 - p2;
+#ifdef FRCNN_BWD_PROF
+#pragma unroll
+            for (int d = 0; d < D; ++d) tp[3] += slow[d] ? 1 : 0;
+#endif
         }
 #ifdef FRCNN_BWD_PROF
         const int gw = (blockIdx.y * gridDim.x + blockIdx.x) * CPW + wid;
@@ -1516,6 +1526,7 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
             g_bwd_prof[gw][1] = tp[1];
             g_bwd_prof[gw][2] = tp[2];
             g_bwd_prof[gw][3] = nr;
+            g_bwd_prof[gw][6] = tp[3];
         }
 #else
         (void)tp;
@@ -1529,6 +1540,15 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
     } else {
         for (int i = lane; i < HW; i += 64) gplane[i] = plane[i];
     }
+#ifdef FRCNN_BWD_PROF
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+    const int gw2 = (blockIdx.y * gridDim.x + blockIdx.x) * CPW + wid;
+    if (lane == 0 && gw2 < kBwdProfWaves) {
+        g_bwd_prof[gw2][4] = t_start;
+        g_bwd_prof[gw2][5] = t_end;
+    }
+#endif
 }
 
 }  // namespace frcnn
@@ -1552,7 +1572,7 @@ extern "C" int frcnn_roi_transform(const float* rois, const float* roi_inds, int
 extern "C" int frcnn_debug_bwd_prof(unsigned long long* out, int reset) {
     (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_prof), sizeof(g_bwd_prof));
     if (reset) {
-        static unsigned long long z[kBwdProfWaves][4];
+        static unsigned long long z[kBwdProfWaves][8];
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bwd_prof), z, sizeof(z));
     }
     return 0;

@@ -36,7 +36,7 @@ def main():
     inds = torch.arange(N, device=dev, dtype=torch.float32).repeat_interleave(S)
     _, am, boxes = ops.roi_pool_head(x, sr, inds, 7, c["img_h"], c["img_w"], rois_sorted=True)
     g = torch.randn(am.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(1))
-    buf = np.zeros((8192, 4), np.uint64)
+    buf = np.zeros((8192, 8), np.uint64)
     res = []
     for rep in range(4):
         torch.cuda.synchronize()
@@ -51,7 +51,21 @@ def main():
             continue
         w = buf[buf[:, 3] > 0].astype(np.float64)
         per = w[:, :3] / w[:, 3:4]
-        res.append({"us": e0.elapsed_time(e1) * 1e3, "waves": int(len(w)),
+        # wave spans on the 100 MHz constant clock (10 ns ticks), relative to the first start
+        t0 = w[:, 4].min()
+        st, en = (w[:, 4] - t0) / 100.0, (w[:, 5] - t0) / 100.0  # us
+        gw = np.arange(len(buf))[buf[:, 3] > 0]  # (by * 16 + bx) * 16 + wid at cfg5 (CPW 16, 16 x 16 grid)
+        img = gw // 256
+        per_img_end = [round(float(en[img == i].max()), 1) for i in range(int(img.max()) + 1)]
+        spans = {"first_start_to_last_end_us": round(float(en.max()), 1),
+                 "start_us_p50_max": [round(float(np.median(st)), 1), round(float(st.max()), 1)],
+                 "span_us_p10_p50_p90_max": [round(float(v), 1) for v in np.percentile(en - st, [10, 50, 90, 100])],
+                 "end_us_p10_p50_p90": [round(float(v), 1) for v in np.percentile(en, [10, 50, 90])],
+                 "per_image_last_end_us": per_img_end,
+                 "per_image_mean_cycles_per_roi": [round(float(w[img == i, :3].sum(1).mean() / w[img == i, 3].mean()), 0)
+                                                   for i in range(int(img.max()) + 1)],
+                 "per_image_flagged_rois": [int(np.median(w[img == i, 6])) for i in range(int(img.max()) + 1)]}
+        res.append({"us": e0.elapsed_time(e1) * 1e3, "waves": int(len(w)), "spans": spans,
                     "cycles_per_roi_mean": [round(float(v), 1) for v in per.mean(0)],
                     "cycles_per_roi_p90": [round(float(v), 1) for v in np.percentile(per, 90, axis=0)],
                     "wave_total_kcycles_mean": round(float(w[:, :3].sum(1).mean() / 1e3), 1)})
