@@ -1270,7 +1270,7 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_pf_kernel(
 constexpr int kBwdProfWaves = 8192;
 // columns: the three phases, the RoI count, then the wave's start and end on the
 // constant 100 MHz clock (s_memrealtime), the end after its plane write-out, then the
-// wave's flagged (ranked) RoIs
+// wave's flagged (ranked) RoIs, and (cycles << 16 | count) of its ring steps holding one
 __device__ unsigned long long g_bwd_prof[kBwdProfWaves][8];
 #define BPROF_T() __builtin_amdgcn_s_memtime()
 #else
@@ -1377,7 +1377,7 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
             mask_load(e, cl_r[d], ch_r[d]);
             asm volatile("" ::: "memory");
         }
-        unsigned long long tp[4] = {0, 0, 0, 0};
+        unsigned long long tp[5] = {0, 0, 0, 0, 0};
         for (int t0 = 0; t0 < nr; t0 += D) {
             const unsigned long long p0 = BPROF_T();
             int nx[D];
@@ -1515,8 +1515,13 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
             tp[1] += p2 - p1;
             tp[2] += p3 - p2;
 #ifdef FRCNN_BWD_PROF
+            bool any_slow = false;
 #pragma unroll
-            for (int d = 0; d < D; ++d) tp[3] += slow[d] ? 1 : 0;
+            for (int d = 0; d < D; ++d) {
+                tp[3] += slow[d] ? 1 : 0;
+                any_slow |= slow[d];
+            }
+            if (any_slow) tp[4] += ((p3 - p0) << 16) | 1u;  // cycles of steps holding a flagged RoI | count
 #endif
         }
 #ifdef FRCNN_BWD_PROF
@@ -1527,6 +1532,7 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
             g_bwd_prof[gw][2] = tp[2];
             g_bwd_prof[gw][3] = nr;
             g_bwd_prof[gw][6] = tp[3];
+            g_bwd_prof[gw][7] = tp[4];
         }
 #else
         (void)tp;

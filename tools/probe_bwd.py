@@ -65,6 +65,15 @@ def main():
                  "per_image_mean_cycles_per_roi": [round(float(w[img == i, :3].sum(1).mean() / w[img == i, 3].mean()), 0)
                                                    for i in range(int(img.max()) + 1)],
                  "per_image_flagged_rois": [int(np.median(w[img == i, 6])) for i in range(int(img.max()) + 1)]}
+        # ring steps (D RoIs each) holding a flagged RoI vs the others, cycles per step
+        raw7 = buf[buf[:, 3] > 0][:, 7]
+        fl_cyc, fl_n = (raw7 >> np.uint64(16)).astype(np.float64), (raw7 & np.uint64(0xFFFF)).astype(np.float64)
+        steps = np.ceil(w[:, 3] / 4.0)  # D = 4
+        tot = w[:, :3].sum(1)
+        has = fl_n > 0
+        spans["cycles_per_step_flagged_vs_plain"] = [
+            round(float(fl_cyc[has].sum() / fl_n[has].sum()), 0),
+            round(float((tot - fl_cyc).sum() / (steps - fl_n).sum()), 0)]
         res.append({"us": e0.elapsed_time(e1) * 1e3, "waves": int(len(w)), "spans": spans,
                     "cycles_per_roi_mean": [round(float(v), 1) for v in per.mean(0)],
                     "cycles_per_roi_p90": [round(float(v), 1) for v in np.percentile(per, 90, axis=0)],
