@@ -224,6 +224,92 @@ def make_input_sets(cfg, images, device, n_sets):
     return c, sets, per
 
 
+# ------------------------------------------------------------- GPU clock state
+class GpuState:
+    """The GPU's clock / power state (amdsmi, else sysfs), so that a slow box can be
+    told apart from a regression: current / min / max GFX and memory clocks, the
+    power cap and draw, and the firmware's recent averages and throttle flags.
+    open() finds the device (before the sampled work is queued), sample() reads it
+    (while the work runs).  Never raises: failures land in the record as "error"."""
+
+    def __init__(self, dev_index):
+        self.h = self.smi = self.dpath = None
+        self.err = None
+        try:
+            p = torch.cuda.get_device_properties(dev_index)
+            self.want = "%04x:%02x:%02x" % (getattr(p, "pci_domain_id", 0), p.pci_bus_id, p.pci_device_id)
+        except Exception:  # noqa: BLE001
+            self.want = None
+        try:
+            import amdsmi
+            amdsmi.amdsmi_init(amdsmi.AmdSmiInitFlags.INIT_AMD_GPUS)
+            self.smi = amdsmi
+            hs = amdsmi.amdsmi_get_processor_handles()
+            for cand in hs:
+                if self.want and str(amdsmi.amdsmi_get_gpu_device_bdf(cand)).lower().startswith(self.want):
+                    self.h = cand
+            if self.h is None and len(hs) == 1:
+                self.h = hs[0]
+            if self.h is None:
+                self.err = f"amdsmi: no handle for {self.want} ({len(hs)} GPUs)"
+        except Exception as e:  # noqa: BLE001
+            self.err = f"amdsmi: {str(e)[:120]}"
+        if self.h is None:
+            import glob
+            for d in glob.glob("/sys/class/drm/card*/device"):
+                if self.want and os.path.basename(os.path.realpath(d)).lower().startswith(self.want):
+                    self.dpath = d
+
+    def sample(self):
+        if self.h is not None:
+            smi, h = self.smi, self.h
+            out = {"source": "amdsmi", "bdf": str(smi.amdsmi_get_gpu_device_bdf(h))}
+
+            def get(key, fn, keep=None):
+                try:
+                    d = fn()
+                    out[key] = {k: (v[:8] if isinstance(v, list) else v) for k, v in d.items()
+                                if keep is None or k in keep}
+                except Exception as e:  # noqa: BLE001
+                    out[key] = {"error": str(e)[:80]}
+            get("gfx_clk_mhz", lambda: smi.amdsmi_get_clock_info(h, smi.AmdSmiClkType.GFX),
+                ("clk", "min_clk", "max_clk", "clk_locked"))
+            get("mem_clk_mhz", lambda: smi.amdsmi_get_clock_info(h, smi.AmdSmiClkType.MEM),
+                ("clk", "min_clk", "max_clk", "clk_locked"))
+            get("power_w", lambda: smi.amdsmi_get_power_info(h),
+                ("current_socket_power", "average_socket_power", "power_limit"))
+            get("power_cap_uw", lambda: smi.amdsmi_get_power_cap_info(h),
+                ("power_cap", "default_power_cap", "min_power_cap", "max_power_cap"))
+            get("metrics", lambda: smi.amdsmi_get_gpu_metrics_info(h),
+                ("average_gfxclk_frequency", "current_gfxclk", "current_gfxclks", "current_uclk",
+                 "average_socket_power", "current_socket_power", "temperature_hotspot", "temperature_mem",
+                 "throttle_status", "indep_throttle_status", "gfxclk_lock_status", "average_gfx_activity",
+                 "average_umc_activity"))
+            return out
+        if self.dpath:
+            import glob
+            out = {"source": "sysfs", "bdf": os.path.basename(os.path.realpath(self.dpath)), "amdsmi": self.err}
+            for f in ("pp_dpm_sclk", "pp_dpm_mclk"):
+                try:
+                    out[f] = open(os.path.join(self.dpath, f)).read().strip().split("\n")[:16]
+                except OSError:
+                    pass
+            for f in glob.glob(os.path.join(self.dpath, "hwmon", "hwmon*", "power1_*")):
+                try:
+                    out[os.path.basename(f)] = open(f).read().strip()
+                except OSError:
+                    pass
+            return out
+        return {"error": self.err or "no device found"}
+
+    def close(self):
+        if self.smi is not None:
+            try:
+                self.smi.amdsmi_shut_down()
+            except Exception:  # noqa: BLE001
+                pass
+
+
 # ------------------------------------------------------------- CPU baseline
 def _host_info():
     model = "unknown"
@@ -528,6 +614,7 @@ def inference_step_fn(args, c, sets, base, world, n_total, backend, ev):
             gather_after(j)
         return cnt
     step.gathered = gathered
+    step.prop_out, step.pool_outs = prop_out, pool_outs  # (parity test: the per-stream buffers)
 
     def alone():  # the dominant kernel by itself (after the timed steps): the last proposals
         ops.roi_pool_head(sets[0][2], prop_out[0][0].view(-1, 4), inds, 7, c["img_h"], c["img_w"],
@@ -763,6 +850,14 @@ def main():
     a1.record()
     torch.cuda.synchronize()
     alone_ms = a0.elapsed_time(a1) / n_alone
+    clocks = None
+    if rank == 0:  # the clock / power state under the same kernel: sampled while ~20 ms of it run
+        gs = GpuState(dev_index)
+        for _ in range(max(50, int(20.0 / max(alone_ms, 1e-3)))):
+            step.alone()
+        clocks = gs.sample()
+        torch.cuda.synchronize()
+        gs.close()
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "roi_pool_bwd_traffic.json" if train
                          else "roi_pool_fwd_traffic.json")
@@ -777,6 +872,7 @@ def main():
                  "kernel_us_alone": alone_ms * 1e3,
                  "frac_alone": alg_bytes / (alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                  "alone_launches": n_alone,
+                 "gpu_state_during_alone": clocks,
                  "event_interval_us_in_pipeline": ev_ms * 1e3}
     if train:
         # the training step's critical path is not an HBM kernel: the target

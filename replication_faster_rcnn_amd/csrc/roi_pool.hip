@@ -1625,21 +1625,28 @@ struct PxPlan {
 };
 constexpr size_t kWaveScratch = 256;  // the wave kernel's reduction scratch + work counter
 constexpr size_t kGeoCap = 368;       // RoIs per geometry chunk (see px_plan)
-PxPlan px_plan(int C, int N, int H, int W, int PHW, hipStream_t st, size_t per_geo = sizeof(int4)) {
+PxPlan px_plan(int C, int N, int H, int W, int PH, int PW, hipStream_t st, size_t per_geo = sizeof(int4)) {
     PxPlan pl;
     const size_t HW = static_cast<size_t>(H) * W;
+    const int PHW = PH * PW;
     if (N <= 0 || HW == 0 || PHW > 64 || H > 65535 || W > 65535) return pl;
     constexpr size_t kReserve = 1024;  // allocation rounding
     const size_t kMinGeo = 64 * per_geo;
     const size_t HWs = (HW + 16) & ~static_cast<size_t>(15);  // + the zero sentinel pixel
+    auto fits = [&](size_t tile) {  // workgroups per CU for a tile of `tile` bytes (0: none)
+        if (2 * (tile + kMinGeo + kWaveScratch + kReserve) <= kLdsPerCu) return 2;
+        return tile + kMinGeo + kWaveScratch + kReserve <= kLdsPerCu ? 1 : 0;
+    };
     for (int cg : {16, 8, 4}) {
         if (C % cg != 0) continue;
         if (path_cfg().roi_cg && cg != path_cfg().roi_cg) continue;  // A/B override
-        const bool kps = cg == 16 && PHW == 49 && HWs <= static_cast<size_t>(kFixPx);
-        const size_t tile = static_cast<size_t>(cg / 4) * (kps ? kFixPx : HWs) * sizeof(float4);
-        int per_cu = 0;
-        if (2 * (tile + kMinGeo + kWaveScratch + kReserve) <= kLdsPerCu) per_cu = 2;
-        else if (tile + kMinGeo + kWaveScratch + kReserve <= kLdsPerCu) per_cu = 1;
+        const size_t tile_rt = static_cast<size_t>(cg / 4) * HWs * sizeof(float4);
+        // The compile-time plane stride instantiates FIX = 7 (7x7 bins, not any 49-bin
+        // shape), and its 153.6 KB tile holds the CU alone: take it only where the
+        // run-time stride would also get one workgroup per CU.
+        const bool kps = cg == 16 && PH == 7 && PW == 7 && HWs <= static_cast<size_t>(kFixPx) && fits(tile_rt) == 1;
+        const size_t tile = kps ? static_cast<size_t>(cg / 4) * kFixPx * sizeof(float4) : tile_rt;
+        const int per_cu = fits(tile);
         if (!per_cu) continue;
         const size_t geo = (kLdsPerCu / per_cu - kReserve - kWaveScratch - tile) / per_geo;
         // geometry chunk: at most kGeoCap RoIs, so that a 16-plane workgroup leaves
@@ -1662,6 +1669,7 @@ int px_launch(const PxPlan& pl, const float* x, const float* rois, int64_t R, in
               int PH, int PW, float ss, float* out, int32_t* argmax, const HeadArgs& hd, hipStream_t st) {
     const dim3 grid(static_cast<unsigned>(C / pl.cg), static_cast<unsigned>(pl.split), static_cast<unsigned>(N + 1));
     const bool fix7 = PH == 7 && PW == 7;
+    FRCNN_REQUIRE(!pl.kps || fix7, "roi_pool_fwd: fixed-stride plan for a non-7x7 output");
 #define FRCNN_PX(CG, FX, KP)                                                                                    \
     do {                                                                                                         \
         if (path_cfg().roi_store)                                                                                \
@@ -1759,7 +1767,7 @@ FwdChoice choose_fwd(int N, int C, int H, int W, int PH, int PW, bool sorted, hi
     const int PHW = PH * PW;
     if (sorted && C > 0) {
         if ((path == kPathAuto || path == kPathWave) &&
-            (ch.px = px_plan(C, N, H, W, PHW, st)).cg) {
+            (ch.px = px_plan(C, N, H, W, PH, PW, st)).cg) {
             ch.kind = kFwdWave;
             return ch;
         }
@@ -1849,7 +1857,7 @@ extern "C" int frcnn_roi_pool_fwd_kernel(int64_t R, int N, int C, int H, int W, 
     int n = 0;
     switch (ch.kind) {
         case kFwdWave:
-            if (ch.px.kps)
+            if (ch.px.kps)  // kps implies the 7x7 head (px_plan)
                 n = snprintf(name, len, "roi_pool_fwd_wave_kernel<1024, %d, %d, %s, %s, %d>", ch.px.cg, fx, hb,
                              path_cfg().roi_store ? "true" : "false", kFixPx * 16);
             else

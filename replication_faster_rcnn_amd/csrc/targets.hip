@@ -312,7 +312,8 @@ struct WalkLds {
     uint32_t ring[kRing][kMtN];   // raw state blocks (the twist's input, the state handed back)
     uint32_t tring[kRing][kMtN];  // the same words tempered (what the walkers read)
     int4 rec[2][kSampWaves];  // per wave, by round parity: (accepted words, margin down, margin up, base)
-    int last[kSampWaves];     // per wave: highest accepted word + 1
+    int last[kSampWaves];     // per wave: highest accepted word + 1 (the window that ends a call)
+    int seq[2][2];            // one-wave walk, by window parity: (step left, words used)
 };
 
 __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
@@ -474,13 +475,13 @@ __device__ void fy_walk(WalkLds& S, Stream& st, int i_hi, int rec_lo, int* J) {
                     SPROF_ADD(9, 1);
                 }
                 if (lane == 0) {  // (double-buffered by the parity: no closing barrier)
-                    S.last[2 * (par & 1)] = i_loc;
-                    S.last[2 * (par & 1) + 1] = used;
+                    S.seq[par & 1][0] = i_loc;
+                    S.seq[par & 1][1] = used;
                 }
             }
             __syncthreads();
             SPROF_DT(10);
-            const int i_new = S.last[2 * (par & 1)], consumed = S.last[2 * (par & 1) + 1];
+            const int i_new = S.seq[par & 1][0], consumed = S.seq[par & 1][1];
             par ^= 1;
             i_cur = i_new;
             if (gen) ++st.ngen;

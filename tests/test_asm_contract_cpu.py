@@ -87,3 +87,16 @@ def test_lead_kernel_no_scratch(asm):
         assert m, sym
         size = re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", m.group(1))
         assert size and int(size.group(1)) == 0, f"{sym} uses scratch (spills)"
+
+
+def test_wave_kernel_no_static_lds(asm):
+    """roi_pool_fwd_wave_kernel decodes argmax from absolute LDS byte addresses of its
+    dynamic tile, which starts at 0 only while the kernel declares no static
+    __shared__: every instantiation's fixed group segment is 0."""
+    syms = {s for s, _ in kernels(asm, "roi_pool_fwd_wave_kernel")}
+    assert syms, "roi_pool_fwd_wave_kernel not found in the ISA"
+    for sym in syms:
+        m = re.search(r"\.amdhsa_kernel " + re.escape(sym) + r"\n(.*?)\.end_amdhsa_kernel", asm, re.S)
+        assert m, sym
+        size = re.search(r"\.amdhsa_group_segment_fixed_size (\d+)", m.group(1))
+        assert size and int(size.group(1)) == 0, f"{sym} declares static LDS"

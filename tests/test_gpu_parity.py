@@ -296,13 +296,16 @@ def _special_x(r, N=2, C=16, H=12, W=14):
     return x
 
 
+@pytest.mark.parametrize("hw", [(12, 14), (38, 38)])
 @pytest.mark.parametrize("fpath,sorted_", FWD_PATHS)
-def test_roi_pool_special_values(fpath, sorted_):
+def test_roi_pool_special_values(fpath, sorted_, hw):
     """Signed zeros, -FLT_MAX, +-inf and NaN inside pooling windows, RoIs partly /
     fully outside the map: every path reproduces the reference's strict-'>'
-    first-max scan bit for bit (values compared as bits)."""
+    first-max scan bit for bit (values compared as bits).  38 x 38 takes the
+    wave kernel's compile-time plane stride (one workgroup per CU), 12 x 14 the
+    run-time stride."""
     r = np.random.default_rng(7)
-    x = _special_x(r)
+    x = _special_x(r, H=hw[0], W=hw[1])
     N = x.shape[0]
     rois = np.array([[b, x1, y1, x1 + w, y1 + h] for b in range(N) for (x1, y1, w, h) in
                      [(0, 0, 13, 11), (1, 2, 5, 3), (3, 3, 0, 0), (2, 1, 9, 9), (-3, -2, 20, 20),
@@ -321,7 +324,7 @@ def test_roi_pool_nontemporal_stores():
     """The wave forward with non-temporal output stores (roi_pool_fwd_store nt):
     the same bits as the oracle, special values included."""
     r = np.random.default_rng(7)
-    x = _special_x(r)
+    x = _special_x(r, H=38, W=38)
     N = x.shape[0]
     rois = np.array([[b, x1, y1, x1 + w, y1 + h] for b in range(N) for (x1, y1, w, h) in
                      [(0, 0, 13, 11), (1, 2, 5, 3), (3, 3, 0, 0), (2, 1, 9, 9), (-3, -2, 20, 20)]], np.float32)
@@ -365,7 +368,8 @@ def _rand_rois(r, b, H, W, lo=-3, span=40):
 @pytest.mark.parametrize("split", ["auto", "1", "3", "64"])
 @pytest.mark.parametrize("case", ["many_images", "invalid_ends", "unsorted", "single_roi", "gaps",
                                   "one_image_tiny_rois", "uniform_sizes", "ph5", "ph8x8", "ph3x9",
-                                  "cfg4_shape", "c8", "c4", "ph1_huge", "ph2_wide"])
+                                  "cfg4_shape", "c8", "c4", "ph1_huge", "ph2_wide",
+                                  "kps_7x7", "kps_1x49", "kps_49x1"])
 def test_roi_pool_tile_cases(case, split, fpath):
     """The image-tile forwards (shape-sorted bins, and RoI-packed "dense"):
     cost-balanced shares (`split` per image), geometry chunks, every window
@@ -374,7 +378,7 @@ def test_roi_pool_tile_cases(case, split, fpath):
     any RoI order (per-image lists) -- bit-exact vs the oracle."""
     r = np.random.default_rng(sum(map(ord, case)))
     ph, pw = {"ph5": (5, 5), "ph8x8": (8, 8), "ph3x9": (3, 9), "ph1_huge": (1, 1),
-              "ph2_wide": (2, 3)}.get(case, (7, 7))
+              "ph2_wide": (2, 3), "kps_1x49": (1, 49), "kps_49x1": (49, 1)}.get(case, (7, 7))
     N, C, H, W = 4, 16, 20, 27
     span = 40
     sorted_ = case != "unsorted"
@@ -401,6 +405,10 @@ def test_roi_pool_tile_cases(case, split, fpath):
         b = np.zeros(500, int)
     elif case == "one_image_tiny_rois":  # > one geometry chunk per workgroup
         N, b, span = 1, np.zeros(6000, int), 2
+    elif case.startswith("kps_"):  # a map whose 16-plane tile holds the CU alone: the fixed
+        # plane stride for 7x7 only, never for the other 49-bin shapes
+        N, C, H, W = 2, 16, 38, 38
+        b = np.sort(r.integers(0, N, 400))
     elif case in ("c8", "c4"):
         C = 8 if case == "c8" else 12
         b = np.sort(r.integers(0, N, 300))
@@ -414,6 +422,9 @@ def test_roi_pool_tile_cases(case, split, fpath):
     with _lib.kernel_path("roi_pool_split", split), _lib.kernel_path("roi_pool_fwd", fpath):
         out, am = ops.roi_pool_with_argmax(torch.from_numpy(x).to(DEV), torch.from_numpy(rois).to(DEV),
                                            (ph, pw), rois_sorted=sorted_)
+        if case.startswith("kps_"):
+            kn = _lib.roi_pool_fwd_kernel(len(b), N, C, H, W, ph, pw, head=False)
+            assert kn.endswith(", 38400>") == (case == "kps_7x7" and fpath == "wave"), kn
     oo, oa = orc.roi_pool_forward(x, rois, (ph, pw))
     valid = (b >= 0) & (b < N)
     assert np.array_equal(am.cpu().numpy()[valid], oa[valid])
