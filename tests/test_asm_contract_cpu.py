@@ -1,6 +1,6 @@
-"""The leader backward's split LDS exchange (roi_pool.hip, roi_pool_bwd_lead_kernel):
-pair k+1's 16 `ds_read_b64` are issued in one asm statement and waited for in a
-later one (`s_waitcnt lgkmcnt(0)` with the same registers as "+v" operands).  The
+"""The leader backwards' split LDS exchange (roi_pool.hip, roi_pool_bwd_lead_kernel /
+roi_pool_bwd_band_kernel): pair k+1's 16 `ds_read_b64` (the band kernel: RoI t+1's 8)
+are issued in one asm statement and waited for in a later one (`s_waitcnt lgkmcnt(0)` with the same registers as "+v" operands).  The
 hardware has no VGPR interlock on LDS returns, so the contract is that nothing
 between the issue and the wait reads, copies or overwrites the destination
 registers, and that the kernel spills nothing.  This test compiles roi_pool.hip
@@ -54,20 +54,23 @@ def asm(tmp_path_factory):
     return out.read_text()
 
 
-def test_lead_kernel_exchange_contract(asm):
-    ks = kernels(asm, "roi_pool_bwd_lead_kernel")
-    assert ks, "roi_pool_bwd_lead_kernel not found in the ISA"
+@pytest.mark.parametrize("name,nread", [("roi_pool_bwd_lead_kernel", 16), ("roi_pool_bwd_band_kernel", 8)])
+def test_bwd_kernel_exchange_contract(asm, name, nread):
+    """The leader kernel exchanges two RoIs per issue (16 reads), the band kernel one (8)."""
+    ks = kernels(asm, name)
+    assert ks, f"{name} not found in the ISA"
     checked = 0
     for sym, body in ks:
         code = [l.split(";")[0].strip() for l in body]
         i = 0
         while i < len(code):
-            if code[i].startswith("ds_read_b64") and i + 15 < len(code) and \
-                    all(code[i + k].startswith("ds_read_b64") for k in range(16)):
+            if code[i].startswith("ds_read_b64") and i + nread - 1 < len(code) and \
+                    all(code[i + k].startswith("ds_read_b64") for k in range(nread)) and \
+                    (i == 0 or not code[i - 1].startswith("ds_read_b64")):
                 dst = set()
-                for k in range(16):
+                for k in range(nread):
                     dst |= regs(code[i + k].split(",")[0])
-                j = i + 16
+                j = i + nread
                 while j < len(code) and not code[j].startswith("s_waitcnt lgkmcnt(0)"):
                     touched = regs(code[j]) & dst
                     assert not touched, f"{sym}: '{code[j]}' touches exchange registers {sorted(touched)} " \
@@ -78,11 +81,12 @@ def test_lead_kernel_exchange_contract(asm):
                 i = j
             else:
                 i += 1
-    assert checked > 0, "no 16-read exchange block found"
+    assert checked > 0, f"no {nread}-read exchange block found"
 
 
-def test_lead_kernel_no_scratch(asm):
-    for sym in {s for s, _ in kernels(asm, "roi_pool_bwd_lead_kernel")}:
+@pytest.mark.parametrize("name", ["roi_pool_bwd_lead_kernel", "roi_pool_bwd_band_kernel"])
+def test_bwd_kernel_no_scratch(asm, name):
+    for sym in {s for s, _ in kernels(asm, name)}:
         m = re.search(r"\.amdhsa_kernel " + re.escape(sym) + r"\n(.*?)\.end_amdhsa_kernel", asm, re.S)
         assert m, sym
         size = re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", m.group(1))

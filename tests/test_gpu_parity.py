@@ -5,6 +5,7 @@ argmax bit-exact; decoded boxes within 1e-5 relative (fp32 exp is
 host-dependent in the reference); RoIPool gradients bit-exact here (the
 kernel reproduces the CPU summation order), 1e-5 relative is the contract.
 """
+import contextlib
 import hashlib
 
 import numpy as np
@@ -524,7 +525,22 @@ def test_roi_pool_head_fused(case):
     assert np.array_equal(xt.grad.cpu().numpy(), og)
 
 
-@pytest.mark.parametrize("path", ["auto", "ring"])
+@contextlib.contextmanager
+def _bwd_path(path):
+    """A backward variant: "bK" = the band kernel with K row bands forced, else a
+    roi_pool_bwd path (auto = the band kernel with its planned bands)."""
+    if path.startswith("b"):
+        with _lib.kernel_path("roi_pool_bwd_bands", path[1:]):
+            yield
+    else:
+        with _lib.kernel_path("roi_pool_bwd", path):
+            yield
+
+
+BWD_VARIANTS = ["auto", "b1", "b2", "b3", "b4", "lead", "ring"]
+
+
+@pytest.mark.parametrize("path", BWD_VARIANTS)
 def test_roi_pool_bwd_ring_equals_plain(path):
     """The latency-hidden backwards (the leader-gather kernel -- the default
     for 7-wide outputs -- and the RoI-at-a-time ring) and the plain
@@ -545,7 +561,7 @@ def test_roi_pool_bwd_ring_equals_plain(path):
     rois = torch.tensor(rows, dtype=torch.float32, device=DEV)
     out, am = ops.roi_pool_with_argmax(x, rois, 7)
     g = torch.randn(out.shape, device=DEV)
-    with _lib.kernel_path("roi_pool_bwd", path):
+    with _bwd_path(path):
         a = _roi_pool_bwd(g, rois, am, x.shape, 1.0)
     with _lib.kernel_path("roi_pool_bwd", "plain"):
         b = _roi_pool_bwd(g, rois, am, x.shape, 1.0)
@@ -554,17 +570,17 @@ def test_roi_pool_bwd_ring_equals_plain(path):
     assert np.array_equal(a.cpu().numpy(), ref)
 
 
-@pytest.mark.parametrize("path", ["auto", "ring", "plain"])
+@pytest.mark.parametrize("path", BWD_VARIANTS + ["plain"])
 def test_roi_pool_bwd_denormal_and_colliding_grads(path):
     """The backward's LDS adds keep IEEE semantics: denormal gradients and sums
     (no flush to zero), many same-pixel contributions (tiny RoIs whose 49 bins
     share a few pixels), signed zeros -- bit-identical to the CPU order."""
     from replication_faster_rcnn_amd.ops import _roi_pool_bwd
     r = np.random.default_rng(11)
-    N, C, H, W = 2, 6, 10, 10
+    N, C, H, W = 2, 6, 16, 10
     x = torch.from_numpy(r.standard_normal((N, C, H, W), dtype=np.float32)).to(DEV)
-    rows = [[0, 2, 2, 2.4, 2.4], [0, 1, 1, 2, 2], [1, 0, 0, 9, 9], [1, 3, 3, 5, 4]] * 5
-    rows += [[b, *r.uniform(0, 9, 2), *r.uniform(0, 9, 2)] for b in (0, 1) for _ in range(9)]
+    rows = [[0, 2, 2, 2.4, 2.4], [0, 1, 1, 2, 2], [1, 0, 0, 9, 15], [1, 3, 3, 5, 4], [0, 4, 7, 5, 8.4]] * 5
+    rows += [[b, *r.uniform(0, 9, 2), *r.uniform(0, 15, 2)] for b in (0, 1) for _ in range(9)]
     rois = torch.tensor(rows, dtype=torch.float32, device=DEV)
     out, am = ops.roi_pool_with_argmax(x, rois, 7)
     g = r.standard_normal(tuple(out.shape)).astype(np.float32)
@@ -572,7 +588,7 @@ def test_roi_pool_bwd_denormal_and_colliding_grads(path):
     g = (g * scale).astype(np.float32)
     g[r.random(g.shape) < 0.05] = -0.0
     assert (np.abs(g[g != 0]) < np.finfo(np.float32).tiny).any()
-    with _lib.kernel_path("roi_pool_bwd", path):
+    with _bwd_path(path):
         gi = _roi_pool_bwd(torch.from_numpy(g).to(DEV), rois, am, x.shape, 1.0)
     ref = orc.roi_pool_backward(g, rois.cpu().numpy(), am.cpu().numpy(), x.shape)
     assert np.array_equal(gi.cpu().numpy().view(np.uint32), ref.view(np.uint32))
@@ -663,7 +679,7 @@ def test_roi_pool_spatial_scale(ss, sorted_):
     assert np.array_equal(gi.cpu().numpy(), orc.roi_pool_backward(gr, rois, oa, x.shape))
 
 
-@pytest.mark.parametrize("path", ["auto", "ring"])
+@pytest.mark.parametrize("path", BWD_VARIANTS)
 def test_roi_pool_bwd_poisoned_workspace(path):
     """The backward's per-image RoI lists are written only up to each image's
     count; the kernels must not read past it.  The cached workspace is filled
@@ -681,7 +697,7 @@ def test_roi_pool_bwd_poisoned_workspace(path):
     ref = orc.roi_pool_backward(gr, rois, oa, x.shape)
     lib = _lib.load()
     need = lib.frcnn_roi_pool_bwd_workspace_size(R, N, 7, 7)
-    with _lib.kernel_path("roi_pool_bwd", path):
+    with _bwd_path(path):
         ws = _lib.cached_workspace("roi_pool_bwd", need, torch.device(DEV))
         ws.fill_(0x7f)
         gi = _roi_pool_bwd(torch.from_numpy(gr).to(DEV), torch.from_numpy(rois).to(DEV),
@@ -700,8 +716,10 @@ def test_roi_pool_fwd_kernel_label():
     assert _lib.roi_pool_fwd_kernel(2000, 1, 512, 50, 84) == "roi_pool_fwd_wave_kernel<1024, 8, 7, true>"
     assert _lib.roi_pool_fwd_kernel(R, N, C, H, W, rois_sorted=False, head=False).startswith(
         "roi_pool_fwd_dense_kernel<1024, 16, 7, false, true>")
-    # the backward's label follows its plan (leader kernel for 7-wide bins, ring / plain on request)
+    # the backward's label follows its plan (band kernel for 7-wide bins, leader / ring / plain on request)
     assert _lib.roi_pool_bwd_kernel(2048, 16, 256, 38, 38) == "roi_pool_bwd_lead_kernel<4, 7>"
+    with _lib.kernel_path("roi_pool_bwd_bands", "2"):
+        assert _lib.roi_pool_bwd_kernel(2048, 16, 256, 38, 38) == "roi_pool_bwd_band_kernel<4, 7>"
     assert _lib.roi_pool_bwd_kernel(2048, 16, 256, 38, 38, 5, 5) == "roi_pool_bwd_pf_kernel<8>"
     with _lib.kernel_path("roi_pool_bwd", "ring"):
         assert _lib.roi_pool_bwd_kernel(2048, 16, 256, 38, 38) == "roi_pool_bwd_pf_kernel<8>"
