@@ -72,11 +72,8 @@ extern "C" int frcnn_set_path(const char* op, const char* path) {
                                        : is(path, "dense")     ? kPathDense
                                                                : kPathWave;
     } else if (is(op, "roi_pool_bwd") &&
-               (aut || is(path, "ring") || is(path, "plain") || is(path, "lead"))) {
-        g_path.roi_bwd = aut ? kPathAuto : is(path, "plain") ? kPathPlain : is(path, "lead") ? kPathLead : kPathRing;
-    } else if (is(op, "roi_pool_bwd_bands") &&
-               (aut || is(path, "1") || is(path, "2") || is(path, "3") || is(path, "4"))) {
-        g_path.roi_bands = aut ? 0 : std::atoi(path);
+               (aut || is(path, "ring") || is(path, "plain"))) {
+        g_path.roi_bwd = aut ? kPathAuto : is(path, "plain") ? kPathPlain : kPathRing;
     } else if (is(op, "propose") &&
                (aut || is(path, "hybrid") || is(path, "lazy") || is(path, "wide"))) {
         g_path.propose = aut ? kPathAuto : is(path, "hybrid") ? kPathHybrid

@@ -20,8 +20,7 @@ constexpr int kPathGeneric = 1;  // roi_pool_fwd: one workgroup per RoI
 constexpr int kPathDense = 2;    // roi_pool_fwd: image tile, RoI bins packed per wave
 constexpr int kPathWave = 3;     // roi_pool_fwd: image tile, one wave per RoI (RoIs grouped by image)
 constexpr int kPathPlain = 1;    // roi_pool_bwd: the unpipelined plane-owner kernel
-constexpr int kPathRing = 2;     // roi_pool_bwd: the RoI-at-a-time ring kernel (auto: band kernel)
-constexpr int kPathLead = 3;     // roi_pool_bwd: the unsplit leader kernel (one wave per plane)
+constexpr int kPathRing = 2;     // roi_pool_bwd: the RoI-at-a-time ring kernel (auto: leader kernel)
 constexpr int kPathHybrid = 1;   // propose: fused per image + chip-wide first-chunk mask
 constexpr int kPathLazy = 2;     // propose: fused per image, lazy NMS from the first chunk on
 constexpr int kPathWide = 3;     // propose: chip-wide sort + bitmask NMS
@@ -34,7 +33,6 @@ struct PathCfg {
     int roi_cg = 0;     // channels per RoIPool workgroup (4 / 8 / 16); 0 = auto
     int sampler = kPathAuto;
     int roi_store = 0;  // RoIPool forward (wave kernel) output stores: 0 temporal (auto), 1 non-temporal
-    int roi_bands = 0;  // RoIPool backward row bands per plane (band kernel); 0 = auto
 };
 const PathCfg& path_cfg();
 

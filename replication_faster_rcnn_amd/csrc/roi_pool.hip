@@ -817,16 +817,10 @@ __global__ __launch_bounds__(256) void roi_transform_kernel(const float* __restr
 // `code` (optional, the backward prep's per-bin codes): entries of RoIs whose
 // bin 0 code has the "slow" bit (overlaps beyond the grid neighbours) get bit
 // 31 set, so the leader backward learns a RoI's path from the scalar list load.
-struct KeepAll {
-    __device__ bool operator()(int) const { return true; }
-};
-// `L` (default b): the list written; `keep(r)`: an extra membership test for
-// image b's RoIs (the band backward's per-band lists).
-template <class Flag, class Keep = KeepAll>
+template <class Flag>
 __device__ __forceinline__ void roi_lists_image(const float* __restrict__ rois, int R, int N, int b,
                                                 int* __restrict__ list, int* __restrict__ cnt, int stride,
-                                                Flag flag_of, int L = -1, Keep keep = Keep()) {
-    if (L < 0) L = b;
+                                                Flag flag_of) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     __shared__ int s_w[16];
     __shared__ int s_last;
@@ -835,7 +829,6 @@ __device__ __forceinline__ void roi_lists_image(const float* __restrict__ rois, 
         int r = r0 + tid;
         int rb = r < R ? static_cast<int>(rois[static_cast<size_t>(r) * stride]) : -1;
         bool m = r < R && (b < N ? rb == b : (rb < 0 || rb >= N));
-        m = m && keep(r);
         uint64_t bal = __ballot(m);
         if (lane == 0) s_w[wid] = __popcll(bal);
         __syncthreads();
@@ -847,16 +840,16 @@ __device__ __forceinline__ void roi_lists_image(const float* __restrict__ rois, 
         if (m) {
             const int flag = flag_of(r) ? static_cast<int>(0x80000000u) : 0;
             const int pos = base + before + __popcll(bal & lanemask_lt());
-            list[static_cast<size_t>(L) * list_stride(R) + pos] = r | flag;
+            list[static_cast<size_t>(b) * list_stride(R) + pos] = r | flag;
             if (pos == base + tot - 1) s_last = r | flag;
         }
         base += tot;
         __syncthreads();
     }
-    if (tid == 0) cnt[L] = base;
+    if (tid == 0) cnt[b] = base;
     // kListPad entries past the last one repeat it, so a reader may fetch whole
     // groups of entries past the image's count without bounds checks
-    if (tid < kListPad) list[static_cast<size_t>(L) * list_stride(R) + base + tid] = base > 0 ? s_last : 0;
+    if (tid < kListPad) list[static_cast<size_t>(b) * list_stride(R) + base + tid] = base > 0 ? s_last : 0;
 }
 
 __global__ __launch_bounds__(1024) void roi_lists_kernel(const float* __restrict__ rois, int R,
@@ -1270,53 +1263,61 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_pf_kernel(
 }
 
 
-// Phase timer of the leader backward (-DFRCNN_BWD_PROF, tools/probe_bwd.py):
-// per wave, shader-clock cycles spent taking / refilling the ring (incl. the
-// load waits), in the neighbour exchanges, and applying to the plane.
+// Phase timer of the leader backward (-DFRCNN_BWD_PROF, tools/probe_bwd_spans.py):
+// per wave, the RoI count, start and end on the constant 100 MHz clock
+// (s_memrealtime, the end after the plane write-out), the flagged RoIs, and the
+// shader-clock cycles of their gathers.
 #ifdef FRCNN_BWD_PROF
 constexpr int kBwdProfWaves = 8192;
-// columns: the three phases, the RoI count, then the wave's start and end on the
-// constant 100 MHz clock (s_memrealtime), the end after its plane write-out, then the
-// wave's flagged (ranked) RoIs, and (cycles << 16 | count) of its ring steps holding one
+// columns: ring+exchange+apply cycles (0-2), RoIs (3), start (4), end (5), flagged
+// RoIs (6), cycles in the flagged RoIs' gathers (7)
 __device__ unsigned long long g_bwd_prof[kBwdProfWaves][8];
-// leader kernel, flagged RoIs only: cycles in the rank walk, its iterations, cycles in
-// the ranked apply rounds, the rounds
-__device__ unsigned long long g_bwd_prof2[kBwdProfWaves][4];
 #define BPROF_T() __builtin_amdgcn_s_memtime()
 #else
 #define BPROF_T() 0ull
 #endif
-constexpr int kBwdXRow = 80;  // leader kernel: exchange-row entries per wave (int2)
-constexpr int kMaxBinsLead = 63;  // leader kernel: PH * PW < 64
+// Exchange row of the leader kernel (int2 (argmax, grad) entries): lane k at entry
+// PW + 1 + k, linear in the lane, so that a wave's reads at any fixed lane offset
+// are bank-conflict free (a layout with a pad entry per bin row, which would drop
+// the grid-edge masks, spreads 32 lanes over > 256 B: 2-way conflicts, op 78 -> 88
+// us at cfg5, profiles/r6_experiments.md).
+constexpr int kBwdXRow = 80;
 
-// Leader-gather plane-owner backward (PH*PW < 64, PW = PWT), the default.
-// Bins that share an argmax pixel all contain it, so their windows overlap;
-// when a RoI's overlaps are only between grid neighbours (the prep kernel's
-// per-RoI flag clear) the bins of one pixel lie in a 2x2 block.  The first of
-// them in bin order (no earlier neighbour -- left, up-left, up, up-right --
-// with the same argmax) leads: it reads the pixel once, adds its own gradient
-// and then those of its later neighbours with the same argmax (right or
-// down-left, down, down-right: ascending bin order) and writes once.  Every
-// pixel so sees the CPU summation order n -> ph -> pw in one read-add-write
-// per RoI, with no rank rounds.  Non-contributing neighbours add -0.0
-// (x + -0.0 == x for every plane value: sums started at +0.0 are never -0.0);
-// non-leaders read and write a dummy word of their own past the plane.  The neighbours'
-// (argmax, grad) pairs come through a per-wave LDS exchange row (one
-// ds_write_b64, eight ds_read_b64 at immediate offsets, conflict free) -- a
-// third of the LDS cycles of twelve ds_bpermute.  RoIs flagged by the prep kernel (tiny
-// windows overlapping beyond the neighbours) rank their bins from the full
-// overlap mask and apply in rounds, as the ring kernel.  D RoIs per step, two
-// per exchange; each pair's read-add-writes go to the plane in RoI order behind
-// the next pair's exchange.
-template <int D, int PWT>
+// Leader-gather plane-owner backward (PH*PW < 64, PW = 7), the default.
+// A wave owns one (image, channel) plane in LDS and walks the image's RoIs in
+// ascending order, lane = bin.  Bins that share an argmax pixel all contain it,
+// so their windows overlap; when a RoI's overlaps are only between grid
+// neighbours (its list entry unflagged) the bins of one pixel lie in a 2x2
+// block.  The first of them in bin order (no earlier neighbour -- left, up-left,
+// up, up-right -- with the same argmax) leads: it reads the pixel once, adds its
+// own gradient and then those of its later neighbours with the same argmax
+// (right or down-left, down, down-right: ascending bin order) and writes once.
+// Every pixel so sees the CPU summation order n -> ph -> pw in one
+// read-add-write per RoI.  Non-contributing neighbours add -0.0 (x + -0.0 == x
+// for every plane value: sums started at +0.0 are never -0.0); non-leaders read
+// and write a dummy word of their own past the plane.  The neighbours' (argmax,
+// grad) pairs come through a per-wave LDS exchange row (one ds_write_b64, eight
+// ds_read_b64 at immediate offsets).  A flagged RoI (tiny windows: bins share a
+// pixel beyond their 2x2 block) gathers instead: every lane reads its pixel and
+// adds the gradient of EVERY bin of the RoI with its argmax, in bin order, from
+// broadcast reads of the row, so all bins of one pixel compute the same CPU-order
+// sum and write the same word (round 6: 1,500 cycles per flagged RoI against
+// ~3,200 for round 5's overlap-mask rank walk + ranked rounds, op 88.7 -> 78.3
+// us at cfg5; profiles/r6_experiments.md).  D RoIs per step, two per exchange;
+// each pair's read-add-writes go to the plane in RoI order behind the next
+// pair's exchange (after it, when the pair holds a flagged RoI: its gather reads
+// the row).  PHT = PH at compile time (the 7x7 head: the gather's reads all
+// issued at once), or 0.
+template <int D, int PWT, int PHT>
 __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
     const float* __restrict__ grad, const int32_t* __restrict__ argmax,
-    const uint64_t* __restrict__ cmask, const uint8_t* __restrict__ code,
     const int* __restrict__ list, const int* __restrict__ cnt,
-    int R, int C, int HW, int HWs, int PHW, int CPW, float* __restrict__ grad_in) {
+    int R, int C, int HW, int HWs, int PH_, int CPW, float* __restrict__ grad_in) {
     extern __shared__ __attribute__((aligned(16))) float planes[];
+    static_assert(PWT == 7, "exchange rows hold 7 bins and a pad");
     constexpr int PW = PWT;
-    static_assert(64 + 2 * (PW + 1) <= kBwdXRow, "exchange row too short");
+    const int PH = PHT > 0 ? PHT : PH_;
+    const int PHW = PH * PW;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int b = blockIdx.y;
@@ -1324,58 +1325,41 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
     if (c >= C) return;  // whole wave; no workgroup barrier below
 #ifdef FRCNN_BWD_PROF
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long tq[2] = {0, 0};
 #endif
     float* gplane = grad_in + (static_cast<size_t>(b) * C + c) * HW;
     // HWs >= HW + 64: word HW + lane is lane's dummy (a word per lane, so the
     // non-leaders' writes do not serialise on one bank)
     float* plane = planes + static_cast<size_t>(wid) * HWs;
-    // Two exchange rows per wave: entry PW + 1 + k holds lane k's pair, linear in the lane so
-    // that a wave's reads at any fixed lane offset are bank-conflict free; a
-    // neighbour across the grid edge is masked by the lane's has_* flags.
-    // (LDS byte addresses; xrow = this lane's entry minus PW + 1 entries, the
-    // up-left neighbour; xbase = lane 0's entry.)
     typedef __attribute__((address_space(3))) float lds_float;
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) const i32x4 lds_i32x4;
+    // this wave's two exchange rows: xbase = lane 0's entry in row 0, xrow = this lane's
+    // entry minus PW + 1 entries (its up-left neighbour); a neighbour across the grid
+    // edge is masked by the lane's has_* flags
+    static_assert(64 + 2 * (PW + 1) <= kBwdXRow, "exchange row too short");
     const uint32_t xbase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_float*)planes)) +
                            static_cast<uint32_t>(CPW * HWs * 4 + wid * 2 * kBwdXRow * 8 + (PW + 1) * 8);
     const uint32_t xrow = xbase + 8 * lane - 8 * (PW + 1);
-    for (int i = lane; i < HWs; i += 64) plane[i] = 0.0f;
-    const int nr = cnt[b];
+    const bool act = lane < PHW;
     const int pw_i = lane % PW;
     const bool has_l = pw_i > 0, has_r = pw_i < PW - 1;
     const bool has_u = lane >= PW, has_d = lane + PW < PHW;
     const bool has_ul = has_u && has_l, has_ur = has_u && has_r;
     const bool has_dl = has_d && has_l, has_dr = has_d && has_r;
+    for (int i = lane; i < HWs; i += 64) plane[i] = 0.0f;
+    const int nr = cnt[b];
     if (nr > 0) {
         const int* lst = list + static_cast<size_t>(b) * list_stride(R);  // wave-uniform: scalar loads
-        const bool act = lane < PHW;
         const uint32_t kl = act ? lane : 0;
         // the host guarantees R*C*PHW*4 < 2^31: byte offsets fit the descriptors
         const uint32_t gb = static_cast<uint32_t>(R) * C * PHW * 4;
-        const uint32_t mb = static_cast<uint32_t>(R) * PHW;
         const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(grad), 0, gb, 0x00020000);
         const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(argmax), 0, gb, 0x00020000);
-        // overlap masks are read only for flagged RoIs, behind a scalar branch on the
-        // (wave-uniform) list entry: a masked-off load through an empty descriptor
-        // still cost its address cycles (cfg5 op 93.3 -> 90.4 us, profiles/r4_experiments.md)
-        const auto rs_m = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(cmask), 0, mb * 8, 0x00020000);
-        auto mask_load = [&](int e, uint32_t& clo, uint32_t& chi) {
-            const uint32_t sm8 = static_cast<uint32_t>(e) * (PHW * 8);
-            clo = chi = 0;
-#if defined(FRCNN_BWD_FLAG_RANKED) && !defined(FRCNN_BWD_RANK_MATCH)
-            if (e < 0) {
-#else
-            if (false) {  // (flagged RoIs gather from the exchange row: no mask)
-#endif
-                const auto m = __builtin_amdgcn_raw_buffer_load_b64(rs_m, kl * 8, sm8, 0);
-                clo = m[0];
-                chi = m[1];
-            }
-        };
         const uint32_t cpb = static_cast<uint32_t>(c) * PHW * 4;
         const uint32_t rpb = static_cast<uint32_t>(C) * PHW * 4;
         int am_r[D], fl_r[D];
         float g_r[D];
-        uint32_t cl_r[D], ch_r[D];
         // list entries: RoI index | flag << 31 (roi_bwd_prep_lists_kernel);
         // the flag drops out of the byte offsets (index x an even stride, mod
         // 2^32).  Positions past the image's RoIs hold copies of its last entry
@@ -1389,15 +1373,9 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
             const uint32_t so = static_cast<uint32_t>(e) * rpb + cpb;
             am_r[d] = __builtin_amdgcn_raw_buffer_load_b32(rs_a, kl * 4, so, 0);
             g_r[d] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g, kl * 4, so, 0));
-            mask_load(e, cl_r[d], ch_r[d]);
             asm volatile("" ::: "memory");
         }
-        unsigned long long tp[5] = {0, 0, 0, 0, 0};
-#ifdef FRCNN_BWD_PROF
-        unsigned long long tq[4] = {0, 0, 0, 0};
-#endif
         for (int t0 = 0; t0 < nr; t0 += D) {
-            const unsigned long long p0 = BPROF_T();
             int nx[D];
 #pragma unroll
             for (int d = 0; d < D; ++d) nx[d] = lst[t0 + D + d];
@@ -1416,12 +1394,11 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
                 const uint32_t so = static_cast<uint32_t>(nx[d]) * rpb + cpb;
                 am_r[d] = __builtin_amdgcn_raw_buffer_load_b32(rs_a, kl * 4, so, 0);
                 g_r[d] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g, kl * 4, so, 0));
+                fl_r[d] = nx[d] < 0;
             }
-            const unsigned long long p1 = BPROF_T();
             // The exchange of slot pair k + 1 is issued before the read-add-writes of pair k
             // and waited for after them: LDS serves a wave in order, so its reads ride in the
-            // shadow of the plane round trips (one exchange round trip per step instead of
-            // D / 2).  The exchange's outputs are tied to the wait by "+v" operands.
+            // shadow of the plane round trips.  The outputs are tied to the wait by "+v" operands.
             static_assert(D % 2 == 0, "slots are exchanged in pairs");
             auto lo = [](uint64_t q) { return static_cast<int>(static_cast<uint32_t>(q)); };
             auto hi = [](uint64_t q) { return __builtin_bit_cast(float, static_cast<uint32_t>(q >> 32)); };
@@ -1468,14 +1445,16 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
                              :
                              : "memory");
             };
-            // A flagged RoI (bins sharing pixels beyond their 2x2 blocks): every lane
-            // reads its pixel once and adds the gradient of EVERY bin of the RoI with
-            // the same argmax, in bin order, from the exchange row (broadcast reads,
-            // -0.0 for the other bins), so all bins of one pixel hold the same CPU-order
-            // sum and write the same word -- no rank, no rounds (round 5: rank walk
-            // ~1,700 + rounds ~1,470 cycles of LDS round trips per flagged RoI,
-            // profiles/r6_experiments.md).  Needs the RoI's row intact: its pair's
-            // next exchange is issued after the applies.
+            auto apply = [&](int d) {
+                float v = plane[addr[d]];
+                v = v + g[d];
+                v = v + s1[d];
+                v = v + s3[d];
+                v = v + s4[d];
+                plane[addr[d]] = v;
+                asm volatile("" ::: "memory");
+            };
+            // flagged RoI d, its pairs in exchange row e: every bin of the RoI, in bin order
             auto apply_gather = [&](int d, int e) {
 #ifdef FRCNN_BWD_PROF
                 const unsigned long long q0 = BPROF_T();
@@ -1483,67 +1462,42 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
                 const int a = am[d];
                 const int ad = a >= 0 ? a : HW + lane;
                 float v = plane[ad];
-                typedef int i32x4 __attribute__((ext_vector_type(4)));
-                typedef __attribute__((address_space(3))) const i32x4 lds_i32x4;
-                const uint32_t row = xbase + e * kBwdXRow * 8;  // lane 0's entry
-                static_assert(64 + PW + 1 >= 8 * ((kMaxBinsLead + 7) / 8), "gather reads past the row");
-                const int npair = (PHW + 1) >> 1;
-                for (int k2 = 0; k2 < npair; k2 += 4) {  // 8 bins per batch of broadcast reads
-                    i32x4 q4[4];
+                const uint32_t row = xbase + e * kBwdXRow * 8;  // lane 0's entry (16-B aligned)
+                // bins 2j, 2j + 1 per broadcast b128 read; entries past the RoI's bins are lanes
+                // >= PHW (argmax -2): never a match.  (__builtin_bit_cast of a vector element .y /
+                // .w read element 0 / 2 here -- a clang miscompile seen in the IR; __int_as_float
+                // of [i] is right)
+                auto pair_add = [&](i32x4 q4) {
+                    v = v + (q4[0] == a ? __int_as_float(q4[1]) : -0.0f);
+                    v = v + (q4[2] == a ? __int_as_float(q4[3]) : -0.0f);
+                };
+                auto pair_read = [&](int j) {
+                    return *reinterpret_cast<lds_i32x4*>(static_cast<size_t>(row + 16 * j));
+                };
+                if constexpr (PHT > 0) {  // every read issued up front, the adds in bin order
+                    constexpr int NQ = (PHT * PW + 1) / 2;
+                    i32x4 qa[NQ];
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        q4[j] = *reinterpret_cast<lds_i32x4*>(static_cast<size_t>(row + 16 * (k2 + j)));
+                    for (int j = 0; j < NQ; ++j) qa[j] = pair_read(j);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        // (entries past the RoI's bins are lanes >= PHW: argmax -2, never a
-                        // match.  __builtin_bit_cast of a vector element .y / .w read element
-                        // 0 / 2 here -- a clang miscompile seen in the IR; __int_as_float of [i]
-                        // is right)
-                        v = v + (q4[j][0] == a ? __int_as_float(q4[j][1]) : -0.0f);
-                        v = v + (q4[j][2] == a ? __int_as_float(q4[j][3]) : -0.0f);
+                    for (int j = 0; j < NQ; ++j) pair_add(qa[j]);
+                } else {
+                    const int nq = (PHW + 1) >> 1;
+                    for (int j0 = 0; j0 < nq; j0 += 4) {  // (reads up to entry 63 + 1: in the row)
+                        i32x4 qa[4];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) qa[j] = pair_read(j0 + j);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) pair_add(qa[j]);
                     }
                 }
                 plane[ad] = v;
-#ifdef FRCNN_BWD_PROF
-                ++tq[3];
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                tq[2] += BPROF_T() - q0;
-#endif
-            };
-            auto apply = [&](int d) {
-                if (!slow[d]) {
-                    float v = plane[addr[d]];
-                    v = v + g[d];
-                    v = v + s1[d];
-                    v = v + s3[d];
-                    v = v + s4[d];
-                    plane[addr[d]] = v;
-                } else {  // ranked rounds, as the ring kernel
-#ifdef FRCNN_BWD_PROF
-                    const unsigned long long q0 = BPROF_T();
-#endif
-                    const int a = am[d];
-                    for (int r = 0;; ++r) {
-#ifdef FRCNN_BWD_PROF
-                        ++tq[3];
-#endif
-#ifdef FRCNN_BWD_FLAG_DSADD
-                        // LDS applies a wave's atomics in issue order: round r's adds land
-                        // before round r + 1's, no read-back between rounds
-                        if (a >= 0 && addr[d] == r)
-                            __hip_atomic_fetch_add(plane + a, g[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
-                        if (a >= 0 && addr[d] == r) plane[a] += g[d];
-#endif
-                        asm volatile("" ::: "memory");
-                        if (__ballot(a >= 0 && addr[d] > r) == 0) break;
-                    }
-#ifdef FRCNN_BWD_PROF
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    tq[2] += BPROF_T() - q0;
-#endif
-                }
                 asm volatile("" ::: "memory");
+#ifdef FRCNN_BWD_PROF
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                tq[0] += 1;
+                tq[1] += BPROF_T() - q0;
+#endif
             };
             x_issue(0);
             x_wait();
@@ -1561,60 +1515,7 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
                     s3[d] = (has_d & (lo(q[e][6]) == a)) ? hi(q[e][6]) : -0.0f;
                     s4[d] = (has_dr & (lo(q[e][7]) == a)) ? hi(q[e][7]) : -0.0f;
                     addr[d] = (a >= 0 && !fol) ? a : HW + lane;
-#ifdef FRCNN_BWD_FLAG_RANKED
-                    if (slow[d]) {  // addr = the bin's rank among the same-pixel bins
-#ifdef FRCNN_BWD_PROF
-                        const unsigned long long q0 = BPROF_T();
-#endif
-#ifdef FRCNN_BWD_RANK_MATCH
-                        // one round per distinct argmax pixel of the RoI: the first pending
-                        // lane's pixel, the ballot of the lanes holding it, their ranks by
-                        // mbcnt -- registers only
-                        int depth = 0;
-                        uint64_t pend = __ballot(a >= 0);
-                        while (pend) {
-#ifdef FRCNN_BWD_PROF
-                            ++tq[1];
-#endif
-                            const int L = __builtin_ctzll(pend);
-                            const int v = __builtin_amdgcn_readlane(a, L);
-                            const uint64_t m = __ballot(a == v);
-                            const int below = static_cast<int>(__builtin_amdgcn_mbcnt_hi(
-                                static_cast<uint32_t>(m >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u)));
-                            depth = a == v ? below : depth;
-                            pend &= ~m;
-                        }
-                        addr[d] = depth;
-#else
-                        int depth = 0;
-                        uint64_t pend = a >= 0 ? ((static_cast<uint64_t>(ch_r[d]) << 32) | cl_r[d]) : 0ull;
-                        const uint32_t xb = xbase + e * kBwdXRow * 8;
-                        while (__ballot(pend != 0)) {
-#ifdef FRCNN_BWD_PROF
-                            ++tq[1];
-#endif
-                            const int p = pend ? __ffsll(static_cast<unsigned long long>(pend)) - 1 : lane;
-                            pend &= pend - 1;
-                            int ap;
-                            asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)"
-                                         : "=v"(ap) : "v"(xb + 8 * p) : "memory");
-                            if (p != lane && ap == a) ++depth;
-                        }
-                        addr[d] = depth;
-#endif
-#ifdef FRCNN_BWD_PROF
-                        tq[0] += BPROF_T() - q0;
-#endif
-                    }
-#endif
-                    mask_load(nx[d], cl_r[d], ch_r[d]);
-                    fl_r[d] = nx[d] < 0;
                 }
-#ifdef FRCNN_BWD_FLAG_RANKED
-                if (d0 + 2 < D) x_issue(d0 + 2);
-                apply(d0);
-                apply(d0 + 1);
-#else
                 if (!(slow[d0] | slow[d0 + 1])) {  // (wave-uniform)
                     if (d0 + 2 < D) x_issue(d0 + 2);
                     apply(d0);
@@ -1626,41 +1527,9 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
                     else apply(d0 + 1);
                     if (d0 + 2 < D) x_issue(d0 + 2);
                 }
-#endif
                 if (d0 + 2 < D) x_wait();
             }
-            const unsigned long long p2 = BPROF_T();
-#ifdef FRCNN_BWD_PROF
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
-            const unsigned long long p3 = BPROF_T();
-            tp[0] += p1 - p0;
-            tp[1] += p2 - p1;
-            tp[2] += p3 - p2;
-#ifdef FRCNN_BWD_PROF
-            bool any_slow = false;
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                tp[3] += slow[d] ? 1 : 0;
-                any_slow |= slow[d];
-            }
-            if (any_slow) tp[4] += ((p3 - p0) << 16) | 1u;  // cycles of steps holding a flagged RoI | count
-#endif
         }
-#ifdef FRCNN_BWD_PROF
-        const int gw = (blockIdx.y * gridDim.x + blockIdx.x) * CPW + wid;
-        if (lane == 0 && gw < kBwdProfWaves) {
-            g_bwd_prof[gw][0] = tp[0];
-            g_bwd_prof[gw][1] = tp[1];
-            g_bwd_prof[gw][2] = tp[2];
-            g_bwd_prof[gw][3] = nr;
-            g_bwd_prof[gw][6] = tp[3];
-            g_bwd_prof[gw][7] = tp[4];
-            for (int k = 0; k < 4; ++k) g_bwd_prof2[gw][k] = tq[k];
-        }
-#else
-        (void)tp;
-#endif
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if ((HW & 3) == 0) {
@@ -1673,258 +1542,15 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
 #ifdef FRCNN_BWD_PROF
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-    const int gw2 = (blockIdx.y * gridDim.x + blockIdx.x) * CPW + wid;
-    if (lane == 0 && gw2 < kBwdProfWaves) {
-        g_bwd_prof[gw2][4] = t_start;
-        g_bwd_prof[gw2][5] = t_end;
-    }
-#endif
-}
-
-
-// Band-split leader backward (PH*PW < 64, PW = PWT): the leader kernel's plane
-// split by rows.  Wave (image b, channel c, band j) owns rows [j*RB, (j+1)*RB)
-// of the (b, c) plane in LDS and walks list b*K + j: the image's RoIs whose
-// bin rows reach the band (roi_bwd_band_lists_kernel), in ascending RoI order.
-// Every pixel has exactly one owner, which applies every RoI's adds to it in
-// the CPU order n -> ph -> pw, so the gradient is bit-identical to the
-// unsplit kernel (and to torchvision's CPU loop); a RoI that crosses a band
-// edge is walked by both owners, each applying only the pixels of its band
-// (argmax outside the band -> -3: never a leader, never applied).  K bands
-// put K x the waves on the chip with 1/K of the plane each (32 waves per CU at
-// cfg5: 8 per SIMD, so <= 64 VGPRs) and cut a wave's serial RoI chain to the
-// RoIs of its band -- the kernel is its slowest waves (profiles/r5_probe_bwd_spans.json).
-// One RoI per exchange (one exchange row per wave): RoI t+1's neighbour
-// exchange is issued before RoI t's read-add-write and waited for after it.
-template <int D, int PWT>
-__global__ __launch_bounds__(1024, 8) void roi_pool_bwd_band_kernel(
-    const float* __restrict__ grad, const int32_t* __restrict__ argmax,
-    const uint64_t* __restrict__ cmask, const int* __restrict__ list, const int* __restrict__ cnt,
-    int R, int C, int H, int W, int K, int RB, int HWs, int PHW, int CPW, float* __restrict__ grad_in) {
-    extern __shared__ __attribute__((aligned(16))) float planes[];
-    constexpr int PW = PWT;
-    static_assert(64 + 2 * (PW + 1) <= kBwdXRow, "exchange row too short");
-    const int lane = threadIdx.x & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int b = blockIdx.y;
-    const int u = blockIdx.x * CPW + wid;  // (channel, band) of the image
-    const int c = u / K, j = u - c * K;
-    if (c >= C) return;  // whole wave; no workgroup barrier below
-    const int p0 = j * RB * W;                          // the band's first pixel
-    const int np = (min((j + 1) * RB, H) - j * RB) * W;  // its pixels (> 0: the host sizes K, RB)
-#ifdef FRCNN_BWD_PROF
-    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-#endif
-    float* gband = grad_in + (static_cast<size_t>(b) * C + c) * H * W + p0;
-    // HWs >= RB * W + 64: word RB * W + lane is lane's dummy
-    float* plane = planes + static_cast<size_t>(wid) * HWs;
-    const int dummy = RB * W + lane;
-    typedef __attribute__((address_space(3))) float lds_float;
-    const uint32_t xbase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_float*)planes)) +
-                           static_cast<uint32_t>(CPW * HWs * 4 + wid * kBwdXRow * 8 + (PW + 1) * 8);
-    const uint32_t xrow = xbase + 8 * lane - 8 * (PW + 1);
-    for (int i = lane; i < HWs; i += 64) plane[i] = 0.0f;
-    const int li = b * K + j;
-    const int nr = cnt[li];
-    const int pw_i = lane % PW;
-    const bool has_l = pw_i > 0, has_r = pw_i < PW - 1;
-    const bool has_u = lane >= PW, has_d = lane + PW < PHW;
-    const bool has_ul = has_u && has_l, has_ur = has_u && has_r;
-    const bool has_dl = has_d && has_l, has_dr = has_d && has_r;
-    unsigned long long tp[5] = {0, 0, 0, 0, 0};
-    if (nr > 0) {
-        const int* lst = list + static_cast<size_t>(li) * list_stride(R);  // wave-uniform: scalar loads
-        const bool act = lane < PHW;
-        const uint32_t kl = act ? lane : 0;
-        const uint32_t gb = static_cast<uint32_t>(R) * C * PHW * 4;
-        const uint32_t mb = static_cast<uint32_t>(R) * PHW;
-        const auto rs_g = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(grad), 0, gb, 0x00020000);
-        const auto rs_a = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(argmax), 0, gb, 0x00020000);
-        const auto rs_m = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(cmask), 0, mb * 8, 0x00020000);
-        const uint32_t cpb = static_cast<uint32_t>(c) * PHW * 4;
-        const uint32_t rpb = static_cast<uint32_t>(C) * PHW * 4;
-        // ring slot d: argmax / grad of a RoI (+ its overlap mask when flagged)
-        int am_r[D];
-        float g_r[D];
-        uint32_t cl_r[D], ch_r[D];
-        int fl_r[D];
-        auto load = [&](int d, int e) {  // e: list entry (RoI index | flag << 31)
-            const uint32_t so = static_cast<uint32_t>(e) * rpb + cpb;
-            am_r[d] = __builtin_amdgcn_raw_buffer_load_b32(rs_a, kl * 4, so, 0);
-            g_r[d] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_g, kl * 4, so, 0));
-            fl_r[d] = e < 0;
-            cl_r[d] = ch_r[d] = 0;
-            if (e < 0) {
-                const auto m = __builtin_amdgcn_raw_buffer_load_b64(rs_m, kl * 8, static_cast<uint32_t>(e) * (PHW * 8), 0);
-                cl_r[d] = m[0];
-                ch_r[d] = m[1];
-            }
-        };
-        // positions past the list's count hold copies of its last entry (kListPad):
-        // their slots are dead (t >= nr -> argmax -1)
-        static_assert(2 * D + 2 <= kListPad, "ring refills read up to 2D + 1 entries past the count");
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            load(d, lst[d]);
-            asm volatile("" ::: "memory");
-        }
-        // the RoI being exchanged / applied
-        int a, fl;
-        float g;
-        uint32_t cl, ch;
-        auto take = [&](int d, int t, int refill) {  // RoI t from slot d, then slot d <- entry `refill`
-            asm volatile("v_mov_b32 %0, %1" : "=v"(a) : "v"(am_r[d]));
-            asm volatile("v_mov_b32 %0, %1" : "=v"(g) : "v"(g_r[d]));
-            asm volatile("v_mov_b32 %0, %1" : "=v"(cl) : "v"(cl_r[d]));
-            asm volatile("v_mov_b32 %0, %1" : "=v"(ch) : "v"(ch_r[d]));
-            fl = t < nr && fl_r[d];
-            int v = t < nr ? a : -1;
-            v = act ? v : -2;
-            const uint32_t rel = static_cast<uint32_t>(v - p0);
-            a = v >= 0 ? (rel < static_cast<uint32_t>(np) ? static_cast<int>(rel) : -3) : v;
-            load(d, refill);
-        };
-        uint64_t q[8];
-        auto lo = [](uint64_t x) { return static_cast<int>(static_cast<uint32_t>(x)); };
-        auto hi = [](uint64_t x) { return __builtin_bit_cast(float, static_cast<uint32_t>(x >> 32)); };
-        auto x_issue = [&]() {
-            const uint64_t m0 = static_cast<uint32_t>(a) | (static_cast<uint64_t>(__builtin_bit_cast(uint32_t, g)) << 32);
-            asm volatile(
-                "ds_write_b64 %8, %9 offset:%c10\n\t"
-                "ds_read_b64 %0, %8 offset:%c11\n\t"
-                "ds_read_b64 %1, %8 offset:%c12\n\t"
-                "ds_read_b64 %2, %8\n\t"
-                "ds_read_b64 %3, %8 offset:%c13\n\t"
-                "ds_read_b64 %4, %8 offset:%c14\n\t"
-                "ds_read_b64 %5, %8 offset:%c15\n\t"
-                "ds_read_b64 %6, %8 offset:%c16\n\t"
-                "ds_read_b64 %7, %8 offset:%c17"
-                : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(q[4]), "=&v"(q[5]), "=&v"(q[6]),
-                  "=&v"(q[7])
-                : "v"(xrow), "v"(m0), "i"(8 * (PW + 1)), "i"(8 * PW), "i"(8), "i"(16), "i"(8 * (PW + 2)),
-                  "i"(8 * (2 * PW)), "i"(8 * (2 * PW + 1)), "i"(8 * (2 * PW + 2))
-                : "memory");
-        };
-        auto x_wait = [&]() {
-            asm volatile("s_waitcnt lgkmcnt(0)"
-                         : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(q[4]), "+v"(q[5]), "+v"(q[6]),
-                           "+v"(q[7])
-                         :
-                         : "memory");
-        };
-        take(0, 0, lst[D]);
-        x_issue();
-        x_wait();
-        for (int t0 = 0; t0 < nr; t0 += D) {
-            const unsigned long long p0t = BPROF_T();
-            int nx[D];
-#pragma unroll
-            for (int d = 0; d < D; ++d) nx[d] = lst[t0 + D + 1 + d];  // refills of this group's takes
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                const int t = t0 + d;
-                // RoI t: leader / followers from the exchange (q: left, up, up-left, up-right,
-                // right, down-left, down, down-right)
-                const bool fol = static_cast<int>(has_l & (lo(q[0]) == a)) | (has_u & (lo(q[1]) == a)) |
-                                 (has_ul & (lo(q[2]) == a)) | (has_ur & (lo(q[3]) == a));
-                const float t5 = (has_dl & (lo(q[5]) == a)) ? hi(q[5]) : -0.0f;
-                const float s1 = (has_r & (lo(q[4]) == a)) ? hi(q[4]) : t5;
-                const float s3 = (has_d & (lo(q[6]) == a)) ? hi(q[6]) : -0.0f;
-                const float s4 = (has_dr & (lo(q[7]) == a)) ? hi(q[7]) : -0.0f;
-                int addr = (a >= 0 && !fol) ? a : dummy;
-                const bool slow = fl;
-                if (slow) {  // addr = the bin's rank among the same-pixel bins (full overlap mask)
-                    int depth = 0;
-                    uint64_t pend = a >= 0 ? ((static_cast<uint64_t>(ch) << 32) | cl) : 0ull;
-                    while (__ballot(pend != 0)) {
-                        const int p = pend ? __ffsll(static_cast<unsigned long long>(pend)) - 1 : lane;
-                        pend &= pend - 1;
-                        int ap;
-                        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)"
-                                     : "=v"(ap) : "v"(xbase + 8 * p) : "memory");
-                        if (p != lane && ap == a) ++depth;
-                    }
-                    addr = depth;
-                }
-                const int ca = a;
-                const float cg = g;
-                // RoI t + 1 from the ring (slot refilled with RoI t + 1 + D), its exchange
-                // issued ahead of RoI t's read-add-write
-                take((d + 1) % D, t + 1, nx[d]);
-                x_issue();
-                if (!slow) {
-                    float v = plane[addr];
-                    v = v + cg;
-                    v = v + s1;
-                    v = v + s3;
-                    v = v + s4;
-                    plane[addr] = v;
-                } else {  // ranked rounds
-                    for (int r = 0;; ++r) {
-                        if (ca >= 0 && addr == r) plane[ca] += cg;
-                        asm volatile("" ::: "memory");
-                        if (__ballot(ca >= 0 && addr > r) == 0) break;
-                    }
-                }
-                asm volatile("" ::: "memory");
-                x_wait();
-#ifdef FRCNN_BWD_PROF
-                tp[3] += slow ? 1 : 0;
-#endif
-            }
-            const unsigned long long p1t = BPROF_T();
-            tp[1] += p1t - p0t;
-        }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    for (int i = lane; i < np; i += 64) gband[i] = plane[i];
-#ifdef FRCNN_BWD_PROF
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
     const int gw = (blockIdx.y * gridDim.x + blockIdx.x) * CPW + wid;
     if (lane == 0 && gw < kBwdProfWaves) {
-        g_bwd_prof[gw][0] = 0;
-        g_bwd_prof[gw][1] = tp[1];
-        g_bwd_prof[gw][2] = 0;
         g_bwd_prof[gw][3] = nr;
         g_bwd_prof[gw][4] = t_start;
         g_bwd_prof[gw][5] = t_end;
-        g_bwd_prof[gw][6] = tp[3];
-        g_bwd_prof[gw][7] = 0;
+        g_bwd_prof[gw][6] = tq[0];
+        g_bwd_prof[gw][7] = tq[1];
     }
-#else
-    (void)tp;
 #endif
-}
-
-// Per-(image, band) RoI lists for the band backward: workgroup L = b * K + j
-// lists image b's RoIs whose bin rows reach rows [j*RB, (j+1)*RB) (windows are
-// monotone in ph: rows [hs(0), he(PH-1)) hold every argmax row), flagged as
-// roi_bwd_prep_lists_kernel flags them; the other workgroups compute the
-// per-RoI overlap masks (16 RoIs each, one wave per RoI).
-__global__ __launch_bounds__(1024) void roi_bwd_band_lists_kernel(const float* __restrict__ rois, int R, int N,
-                                                                  int H, int W, int PH, int PW, float ss, int K,
-                                                                  int RB, uint64_t* __restrict__ cmask,
-                                                                  uint8_t* __restrict__ code, int* __restrict__ list,
-                                                                  int* __restrict__ cnt) {
-    const int L = blockIdx.x;
-    if (L < N * K) {
-        const int b = L / K, j = L - b * K;
-        const int y0 = j * RB, y1 = min((j + 1) * RB, H);
-        roi_lists_image(
-            rois, R, N, b, list, cnt, 5,
-            [&](int r) { return roi_far_overlap(rois + static_cast<size_t>(r) * 5, ss, H, W, PH, PW); },
-            L, [&](int r) {
-                const float* roi = rois + static_cast<size_t>(r) * 5;
-                const RoiGeom g = roi_geom(roi, ss, PH, PW);
-                const int hs = geom_bin(g, H, W, 0, 0).x, he = geom_bin(g, H, W, PH - 1, 0).y;
-                return he > hs && hs < y1 && he > y0;
-            });
-        return;
-    }
-    const int r = (L - N * K) * 16 + (threadIdx.x >> 6);
-    if (r >= R) return;  // whole wave
-    roi_bwd_prep64_roi(rois, r, H, W, PH, PW, ss, cmask, code);
 }
 
 }  // namespace frcnn
@@ -1945,15 +1571,6 @@ extern "C" int frcnn_roi_transform(const float* rois, const float* roi_inds, int
 }
 
 #ifdef FRCNN_BWD_PROF
-extern "C" int frcnn_debug_bwd_prof2(unsigned long long* out, int reset) {
-    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_prof2), sizeof(g_bwd_prof2));
-    if (reset) {
-        static unsigned long long z[kBwdProfWaves][4];
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bwd_prof2), z, sizeof(z));
-    }
-    return 0;
-}
-
 extern "C" int frcnn_debug_bwd_prof(unsigned long long* out, int reset) {
     (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_prof), sizeof(g_bwd_prof));
     if (reset) {
@@ -2284,7 +1901,6 @@ extern "C" int frcnn_roi_pool_fwd_head(const float* x, const float* rois, const 
 }
 
 namespace {
-constexpr int kBwdMaxBands = 4;  // row bands per plane (band kernel)
 struct BwdWs {
     uint64_t* cmask;
     uint8_t* code;
@@ -2297,9 +1913,8 @@ BwdWs carve_bwd(void* ws, int64_t R, int N, int PH, int PW) {
     BwdWs w{};
     w.cmask = c.take<uint64_t>(static_cast<size_t>(R) * PH * PW);
     w.code = c.take<uint8_t>(static_cast<size_t>(R) * PH * PW);
-    // (N + 1 lists for the other kernels; N * K for the band kernel, K <= kBwdMaxBands)
-    w.list = c.take<int>(static_cast<size_t>(N * kBwdMaxBands + 1) * list_stride(R));
-    w.cnt = c.take<int>(N * kBwdMaxBands + 1);
+    w.list = c.take<int>(static_cast<size_t>(N + 1) * list_stride(R));
+    w.cnt = c.take<int>(N + 1);
     w.bytes = c.used();
     return w;
 }
@@ -2311,10 +1926,6 @@ constexpr int kBwdRing = 8;                      // RoIs in flight per wave (rin
 #define FRCNN_BWD_LEAD_D 4
 #endif
 constexpr int kBwdLead = FRCNN_BWD_LEAD_D;                   // RoIs per step (leader kernel)
-#ifndef FRCNN_BWD_BAND_D
-#define FRCNN_BWD_BAND_D 4
-#endif
-constexpr int kBwdBandD = FRCNN_BWD_BAND_D;                  // ring depth (band kernel)
 constexpr size_t kPlaneBudgetRing = 144 * 1024;  // ring kernel: one workgroup per CU
 }  // namespace
 
@@ -2330,12 +1941,10 @@ namespace {
 // CU (ceil(N*C / CUs) waves each) where the LDS allows -- a 2:1 mix of busy and
 // half-idle CUs cost 1.35x.
 struct BwdPlan {
-    bool ring = false, lead = false, band = false;
+    bool ring = false, lead = false;
     int icpw = 1, HWs = 0;
-    int K = 1, RB = 0;  // band kernel: row bands per plane, rows per band
     size_t lead_bytes = 0;
 };
-constexpr size_t kBandLdsPerWg = 80 * 1024;  // band kernel: two workgroups per CU
 BwdPlan bwd_plan(int64_t R, int N, int C, int H, int W, int PH, int PW) {
     BwdPlan pl;
     const size_t HW = static_cast<size_t>(H) * W;
@@ -2355,34 +1964,7 @@ BwdPlan bwd_plan(int64_t R, int N, int C, int H, int W, int PH, int PW) {
         const bool fits = static_cast<uint64_t>(R) * C * PHW * 4 < (1ull << 31);
         pl.HWs = static_cast<int>((HW + 64 + 3) & ~static_cast<size_t>(3));  // + dummy words
         pl.lead_bytes = static_cast<size_t>(pl.icpw) * (pl.HWs * sizeof(float) + 2 * kBwdXRow * 8);
-        pl.lead = fits && (bp == kPathAuto || bp == kPathLead) && PHW < 64 && PW == 7 &&
-                  pl.lead_bytes <= kPlaneBudgetRing;
-        // band kernel (default): the most bands (<= kBwdMaxBands, >= 4 rows each) whose
-        // N * C * K waves are all resident at 32 per CU; 16 waves per workgroup where
-        // two workgroups fit a CU's LDS
-        if (pl.lead && bp != kPathLead && path_cfg().roi_bands) {  // (measured slower: opt-in)
-            const int64_t cap = 32ll * device_cu_count();
-            const int force = path_cfg().roi_bands;
-            for (int K = kBwdMaxBands; K >= 1; --K) {
-                if (force && K != force) continue;
-                const int RB = (H + K - 1) / K;
-                if (K > 1 && (RB < 4 || (K - 1) * RB >= H)) continue;
-                if (!force && K > 1 && static_cast<int64_t>(N) * C * K > cap) continue;
-                const int HWs = (RB * W + 64 + 3) & ~3;
-                const size_t per_wave = static_cast<size_t>(HWs) * 4 + kBwdXRow * 8;
-                int64_t cpw = static_cast<int64_t>(kBandLdsPerWg / per_wave);
-                cpw = cpw > 16 ? 16 : cpw;
-                if (cpw < 1) continue;
-                pl.band = true;
-                pl.K = K;
-                pl.RB = RB;
-                pl.HWs = HWs;
-                pl.icpw = static_cast<int>(cpw);
-                pl.lead_bytes = static_cast<size_t>(cpw) * per_wave;
-                break;
-            }
-            if (pl.band) pl.lead = false;
-        }
+        pl.lead = fits && bp == kPathAuto && PHW < 64 && PW == 7 && pl.lead_bytes <= kPlaneBudgetRing;
     }
     return pl;
 }
@@ -2396,10 +1978,8 @@ extern "C" int frcnn_roi_pool_bwd_kernel(int64_t R, int N, int C, int H, int W, 
     const BwdPlan pl = bwd_plan(R, N, C, H, W, PH, PW);
     const size_t plane_bytes = static_cast<size_t>(H) * W * sizeof(float);
     int n;
-    if (pl.band)
-        n = snprintf(name, len, "roi_pool_bwd_band_kernel<%d, 7>", kBwdBandD);
-    else if (pl.lead)
-        n = snprintf(name, len, "roi_pool_bwd_lead_kernel<%d, 7>", kBwdLead);
+    if (pl.lead)
+        n = snprintf(name, len, "roi_pool_bwd_lead_kernel<%d, 7, %d>", kBwdLead, PH == 7 ? 7 : 0);
     else if (pl.ring)
         n = snprintf(name, len, "roi_pool_bwd_pf_kernel<%d>", kBwdRing);
     else
@@ -2434,24 +2014,8 @@ extern "C" int frcnn_roi_pool_bwd(const float* grad, const float* rois, const in
     const bool ring = pl.ring, lead = pl.lead;
     const int icpw = pl.icpw, HWs = pl.HWs;
     const size_t lead_bytes = pl.lead_bytes;
-    if (pl.band) {  // per-(image, band) lists and the flagged RoIs' masks in one launch
-        const unsigned grid = static_cast<unsigned>(N * pl.K + (R + 15) / 16);
-        hipLaunchKernelGGL(roi_bwd_band_lists_kernel, dim3(grid), dim3(1024), 0, st, rois, static_cast<int>(R), N, H,
-                           W, PH, PW, spatial_scale, pl.K, pl.RB, w.cmask, w.code, w.list, w.cnt);
-        FRCNN_LAUNCH_CHECK("roi_bwd_band_lists_kernel");
-        dim3 grid2((C * pl.K + icpw - 1) / icpw, N);
-        hipLaunchKernelGGL((roi_pool_bwd_band_kernel<kBwdBandD, 7>), grid2, dim3(64 * icpw), lead_bytes, st, grad,
-                           argmax, w.cmask, w.list, w.cnt, static_cast<int>(R), C, H, W, pl.K, pl.RB, HWs, PHW, icpw,
-                           grad_in);
-        FRCNN_LAUNCH_CHECK("roi_pool_bwd_band_kernel");
-        return FRCNN_OK;
-    }
-    if (lead) {  // lists (entries flagged from the geometry); the flagged RoIs need no overlap masks
-#ifdef FRCNN_BWD_FLAG_RANKED
-        const unsigned grid = static_cast<unsigned>(N + 1 + (R + 15) / 16);
-#else
+    if (lead) {  // lists only (entries flagged from the geometry): the flagged RoIs need no overlap masks
         const unsigned grid = static_cast<unsigned>(N + 1);
-#endif
         hipLaunchKernelGGL(roi_bwd_prep_lists_kernel, dim3(grid), dim3(1024), 0, st, rois, static_cast<int>(R), N, H,
                            W, PH, PW, spatial_scale, w.cmask, w.code, w.list, w.cnt);
         FRCNN_LAUNCH_CHECK("roi_bwd_prep_lists_kernel");
@@ -2470,9 +2034,16 @@ extern "C" int frcnn_roi_pool_bwd(const float* grad, const float* rois, const in
     if (ring) {
         dim3 grid((C + icpw - 1) / icpw, N);
         if (lead)
-            hipLaunchKernelGGL((roi_pool_bwd_lead_kernel<kBwdLead, 7>), grid, dim3(64 * icpw), lead_bytes,
-                               st, grad, argmax, w.cmask, w.code, w.list, w.cnt, static_cast<int>(R), C,
-                               static_cast<int>(HW), HWs, PHW, icpw, grad_in);
+        {
+            if (PH == 7)
+                hipLaunchKernelGGL((roi_pool_bwd_lead_kernel<kBwdLead, 7, 7>), grid, dim3(64 * icpw), lead_bytes,
+                                   st, grad, argmax, w.list, w.cnt, static_cast<int>(R), C, static_cast<int>(HW),
+                                   HWs, PH, icpw, grad_in);
+            else
+                hipLaunchKernelGGL((roi_pool_bwd_lead_kernel<kBwdLead, 7, 0>), grid, dim3(64 * icpw), lead_bytes,
+                                   st, grad, argmax, w.list, w.cnt, static_cast<int>(R), C, static_cast<int>(HW),
+                                   HWs, PH, icpw, grad_in);
+        }
         else
             hipLaunchKernelGGL(roi_pool_bwd_pf_kernel<kBwdRing>, grid, dim3(64 * icpw), icpw * plane_bytes, st,
                                grad, argmax, w.cmask, w.code, w.list, w.cnt, static_cast<int>(R), C,

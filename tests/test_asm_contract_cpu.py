@@ -1,6 +1,6 @@
-"""The leader backwards' split LDS exchange (roi_pool.hip, roi_pool_bwd_lead_kernel /
-roi_pool_bwd_band_kernel): pair k+1's 16 `ds_read_b64` (the band kernel: RoI t+1's 8)
-are issued in one asm statement and waited for in a later one (`s_waitcnt lgkmcnt(0)` with the same registers as "+v" operands).  The
+"""The leader backward's split LDS exchange (roi_pool.hip, roi_pool_bwd_lead_kernel):
+pair k+1's 16 `ds_read_b64` are issued in one asm statement and waited for in a
+later one (`s_waitcnt lgkmcnt(0)` with the same registers as "+v" operands).  The
 hardware has no VGPR interlock on LDS returns, so the contract is that nothing
 between the issue and the wait reads, copies or overwrites the destination
 registers, and that the kernel spills nothing.  This test compiles roi_pool.hip
@@ -54,9 +54,9 @@ def asm(tmp_path_factory):
     return out.read_text()
 
 
-@pytest.mark.parametrize("name,nread", [("roi_pool_bwd_lead_kernel", 16), ("roi_pool_bwd_band_kernel", 8)])
+@pytest.mark.parametrize("name,nread", [("roi_pool_bwd_lead_kernel", 16)])
 def test_bwd_kernel_exchange_contract(asm, name, nread):
-    """The leader kernel exchanges two RoIs per issue (16 reads), the band kernel one (8)."""
+    """The leader kernel exchanges two RoIs per issue (16 reads)."""
     ks = kernels(asm, name)
     assert ks, f"{name} not found in the ISA"
     checked = 0
@@ -84,7 +84,7 @@ def test_bwd_kernel_exchange_contract(asm, name, nread):
     assert checked > 0, f"no {nread}-read exchange block found"
 
 
-@pytest.mark.parametrize("name", ["roi_pool_bwd_lead_kernel", "roi_pool_bwd_band_kernel"])
+@pytest.mark.parametrize("name", ["roi_pool_bwd_lead_kernel"])
 def test_bwd_kernel_no_scratch(asm, name):
     for sym in {s for s, _ in kernels(asm, name)}:
         m = re.search(r"\.amdhsa_kernel " + re.escape(sym) + r"\n(.*?)\.end_amdhsa_kernel", asm, re.S)

@@ -64,8 +64,7 @@ def test_set_path_accepts_the_documented_paths_only():
     from replication_faster_rcnn_amd import _lib
     lib = _lib.load(require_gpu=False)
     ok = {"roi_pool_fwd": ["auto", "wave", "dense", "generic"],
-          "roi_pool_bwd": ["auto", "ring", "plain", "lead"],
-          "roi_pool_bwd_bands": ["auto", "1", "2", "3", "4"],
+          "roi_pool_bwd": ["auto", "ring", "plain"],
           "propose": ["auto", "hybrid", "lazy", "wide"],
           "roi_pool_fwd_store": ["auto", "temporal", "nt"],
           "sampler": ["auto", "walk"],
@@ -77,8 +76,7 @@ def test_set_path_accepts_the_documented_paths_only():
                 assert lib.frcnn_set_path(op.encode(), p.encode()) == 0, (op, p)
         for op, p in [("roi_pool_fwd_store", "streaming"), ("roi_pool_split", "65"), ("roi_pool_split", "x"),
                       ("roi_pool_cg", "2"), ("sampler", "tiles"), ("sampler", "chip"), ("roi_pool_fwd", "key"),
-                      ("roi_pool_fwd", "pair"), ("roi_pool_bwd_bands", "5"), ("roi_pool_bwd_bands", "0"),
-                      ("no_such_op", "auto")]:
+                      ("roi_pool_fwd", "pair"), ("roi_pool_bwd", "band"), ("no_such_op", "auto")]:
             assert lib.frcnn_set_path(op.encode(), p.encode()) == -1, (op, p)
             assert p.encode() in lib.frcnn_last_error()
     finally:

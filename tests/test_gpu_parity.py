@@ -5,7 +5,6 @@ argmax bit-exact; decoded boxes within 1e-5 relative (fp32 exp is
 host-dependent in the reference); RoIPool gradients bit-exact here (the
 kernel reproduces the CPU summation order), 1e-5 relative is the contract.
 """
-import contextlib
 import hashlib
 
 import numpy as np
@@ -525,19 +524,7 @@ def test_roi_pool_head_fused(case):
     assert np.array_equal(xt.grad.cpu().numpy(), og)
 
 
-@contextlib.contextmanager
-def _bwd_path(path):
-    """A backward variant: "bK" = the band kernel with K row bands forced, else a
-    roi_pool_bwd path (auto = the band kernel with its planned bands)."""
-    if path.startswith("b"):
-        with _lib.kernel_path("roi_pool_bwd_bands", path[1:]):
-            yield
-    else:
-        with _lib.kernel_path("roi_pool_bwd", path):
-            yield
-
-
-BWD_VARIANTS = ["auto", "b1", "b2", "b3", "b4", "lead", "ring"]
+BWD_VARIANTS = ["auto", "ring"]
 
 
 @pytest.mark.parametrize("path", BWD_VARIANTS)
@@ -561,7 +548,7 @@ def test_roi_pool_bwd_ring_equals_plain(path):
     rois = torch.tensor(rows, dtype=torch.float32, device=DEV)
     out, am = ops.roi_pool_with_argmax(x, rois, 7)
     g = torch.randn(out.shape, device=DEV)
-    with _bwd_path(path):
+    with _lib.kernel_path("roi_pool_bwd", path):
         a = _roi_pool_bwd(g, rois, am, x.shape, 1.0)
     with _lib.kernel_path("roi_pool_bwd", "plain"):
         b = _roi_pool_bwd(g, rois, am, x.shape, 1.0)
@@ -588,7 +575,7 @@ def test_roi_pool_bwd_denormal_and_colliding_grads(path):
     g = (g * scale).astype(np.float32)
     g[r.random(g.shape) < 0.05] = -0.0
     assert (np.abs(g[g != 0]) < np.finfo(np.float32).tiny).any()
-    with _bwd_path(path):
+    with _lib.kernel_path("roi_pool_bwd", path):
         gi = _roi_pool_bwd(torch.from_numpy(g).to(DEV), rois, am, x.shape, 1.0)
     ref = orc.roi_pool_backward(g, rois.cpu().numpy(), am.cpu().numpy(), x.shape)
     assert np.array_equal(gi.cpu().numpy().view(np.uint32), ref.view(np.uint32))
@@ -697,7 +684,7 @@ def test_roi_pool_bwd_poisoned_workspace(path):
     ref = orc.roi_pool_backward(gr, rois, oa, x.shape)
     lib = _lib.load()
     need = lib.frcnn_roi_pool_bwd_workspace_size(R, N, 7, 7)
-    with _bwd_path(path):
+    with _lib.kernel_path("roi_pool_bwd", path):
         ws = _lib.cached_workspace("roi_pool_bwd", need, torch.device(DEV))
         ws.fill_(0x7f)
         gi = _roi_pool_bwd(torch.from_numpy(gr).to(DEV), torch.from_numpy(rois).to(DEV),
@@ -717,9 +704,8 @@ def test_roi_pool_fwd_kernel_label():
     assert _lib.roi_pool_fwd_kernel(R, N, C, H, W, rois_sorted=False, head=False).startswith(
         "roi_pool_fwd_dense_kernel<1024, 16, 7, false, true>")
     # the backward's label follows its plan (band kernel for 7-wide bins, leader / ring / plain on request)
-    assert _lib.roi_pool_bwd_kernel(2048, 16, 256, 38, 38) == "roi_pool_bwd_lead_kernel<4, 7>"
-    with _lib.kernel_path("roi_pool_bwd_bands", "2"):
-        assert _lib.roi_pool_bwd_kernel(2048, 16, 256, 38, 38) == "roi_pool_bwd_band_kernel<4, 7>"
+    assert _lib.roi_pool_bwd_kernel(2048, 16, 256, 38, 38) == "roi_pool_bwd_lead_kernel<4, 7, 7>"
+    assert _lib.roi_pool_bwd_kernel(2048, 16, 256, 38, 38, 9, 7) == "roi_pool_bwd_lead_kernel<4, 7, 0>"
     assert _lib.roi_pool_bwd_kernel(2048, 16, 256, 38, 38, 5, 5) == "roi_pool_bwd_pf_kernel<8>"
     with _lib.kernel_path("roi_pool_bwd", "ring"):
         assert _lib.roi_pool_bwd_kernel(2048, 16, 256, 38, 38) == "roi_pool_bwd_pf_kernel<8>"

@@ -49,13 +49,8 @@ def build(config="cfg5", per_image=128, rois_mode="sampled", dev=None):
 
 
 def set_variant(p):
-    """"bK": the band kernel with K row bands forced; else a roi_pool_bwd path."""
-    if p.startswith("b"):
-        _lib.set_path("roi_pool_bwd", "auto")
-        _lib.set_path("roi_pool_bwd_bands", p[1:])
-    else:
-        _lib.set_path("roi_pool_bwd_bands", "auto")
-        _lib.set_path("roi_pool_bwd", p)
+    """A roi_pool_bwd path (auto = the leader kernel for 7-wide bins)."""
+    _lib.set_path("roi_pool_bwd", p)
 
 
 def main():
@@ -89,7 +84,6 @@ def main():
             torch.cuda.synchronize()
             times[p].append(e0.elapsed_time(e1) / a.iters * 1e3)
     _lib.set_path("roi_pool_bwd", "auto")
-    _lib.set_path("roi_pool_bwd_bands", "auto")
     res = {p: {"us_median": float(np.median(t)), "GBps": alg / (np.median(t) * 1e-6) / 1e9,
                "frac": alg / (np.median(t) * 1e-6) / 8e12} for p, t in times.items()}
     print(json.dumps({"config": a.config, "R": R, "alg_bytes": alg, "paths": res}, indent=1))

@@ -1,11 +1,11 @@
-"""Per-wave spans of the leader / band RoIPool backward from a -DFRCNN_BWD_PROF
+"""Per-wave spans of the leader RoIPool backward from a -DFRCNN_BWD_PROF
 build, on the training-step inputs of tools/ab_roi_pool_bwd.py (ProposalTarget's
 128 sampled RoIs per image): wave start / end on the 100 MHz constant clock,
 RoIs walked and flagged RoIs per wave, and what the slowest waves hold.
 
     make -C replication_faster_rcnn_amd/csrc BUILD=build_bp EXTRA=-DFRCNN_BWD_PROF \\
         OUT=../../tools/prev/libfrcnn_BP.so
-    FRCNN_LIB_PATH=$PWD/tools/prev/libfrcnn_BP.so python tools/probe_bwd_spans.py --variants lead,b2
+    FRCNN_LIB_PATH=$PWD/tools/prev/libfrcnn_BP.so python tools/probe_bwd_spans.py --variants auto
 """
 import argparse
 import ctypes
@@ -24,38 +24,32 @@ from replication_faster_rcnn_amd import _lib, ops  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="lead,b2")
+    ap.add_argument("--variants", default="auto")
     a = ap.parse_args()
     lib = _lib.load()
     fn = lib.frcnn_debug_bwd_prof
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    fn2 = getattr(lib, "frcnn_debug_bwd_prof2", None)
-    if fn2 is not None:
-        fn2.restype = ctypes.c_int
-        fn2.argtypes = [ctypes.c_void_p, ctypes.c_int]
+
     g, boxes, am, xs = build()
     N, C, H, W = xs
     out = {}
     for v in a.variants.split(","):
         set_variant(v)
-        K = int(v[1:]) if v.startswith("b") else 1
+        K = 1
         buf = np.zeros((8192, 8), np.uint64)
         runs = []
         for rep in range(3):
             torch.cuda.synchronize()
             fn(buf.ctypes.data, 1)
-            buf2 = np.zeros((8192, 4), np.uint64)
-            if fn2 is not None:
-                fn2(buf2.ctypes.data, 1)
+
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             ops._roi_pool_bwd(g, boxes, am, xs, 1.0)
             e1.record()
             torch.cuda.synchronize()
             fn(buf.ctypes.data, 0)
-            if fn2 is not None:
-                fn2(buf2.ctypes.data, 0)
+
             gw = np.nonzero(buf[:, 5] > 0)[0]
             w = buf[gw].astype(np.float64)
             t0 = w[:, 4].min()
@@ -63,13 +57,8 @@ def main():
             img = gw // (C * K)
             span = en - st
             slow = np.argsort(span)[-32:]
-            q = buf2[gw].astype(np.float64)
             nfl = np.maximum(w[:, 6], 1)
-            flagged = {"rank_cycles_per_flagged": round(float((q[:, 0] / nfl).mean()), 0),
-                       "rank_iters_per_flagged": round(float((q[:, 1] / nfl).mean()), 2),
-                       "round_cycles_per_flagged": round(float((q[:, 2] / nfl).mean()), 0),
-                       "rounds_per_flagged": round(float((q[:, 3] / nfl).mean()), 2),
-                       "loop_cycles_per_roi": round(float((w[:, :3].sum(1) / np.maximum(w[:, 3], 1)).mean()), 0)}
+            flagged = {"gather_cycles_per_flagged": round(float((w[:, 7] / nfl).mean()), 0)}
             runs.append({"op_us": round(e0.elapsed_time(e1) * 1e3, 1), "waves": int(len(gw)), "flagged_detail": flagged,
                          "span_us_p10_p50_p90_max": [round(float(x), 1) for x in np.percentile(span, [10, 50, 90, 100])],
                          "last_end_us": round(float(en.max()), 1),
