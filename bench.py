@@ -758,6 +758,40 @@ def train_step_fn(args, c, sets, base, first_image, ev):
     return step
 
 
+def strong_cfg3(args, world, rank, dev, backend, base_of):
+    """BASELINE configs[2] as written: the 64-image batch sharded per image over the
+    N ranks (strong scaling), timed like the headline (barrier + sync on both sides,
+    max over ranks).  Reported beside the weak-scaled cfg2 line for N > 1."""
+    from replication_faster_rcnn_amd import dist as fdist
+    from replication_faster_rcnn_amd import synth
+    n_total = synth.CONFIGS["cfg3"]["batch"]
+    mine = fdist.shard(n_total, rank, world)
+    c, sets, _ = make_input_sets("cfg3", mine, dev, min(args.input_sets or 4, 4))
+    base = base_of.generate_anchor_base_device(anchor_scales=c["scales"])
+    ev = {"fwd": [], "bwd": [], "draw": [], "i": 0,
+          "pairs": [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    for _ in range(args.steps)]}
+    step = inference_step_fn(args, c, sets, base, world, n_total, backend, ev)
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    return {"workload": f"cfg3: {n_total} images sharded per image over {world} ranks (BASELINE configs[2])",
+            "value": n_total * args.steps / el, "unit": "images/sec", "ms_per_step": el / args.steps * 1e3,
+            "scaling": "strong", "global_batch": n_total, "images_per_gpu_max": len(mine)}
+
+
 def main():
     args = parse()
     maybe_launch(args)
@@ -917,6 +951,13 @@ def main():
     }
     if gathered:
         rec["gathered_last_step"] = gathered
+    if world > 1 and args.config == "auto" and not args.host_io:
+        # configs[2] as written (64 GLOBAL images sharded per image, strong scaling),
+        # beside the weak-scaled headline: the same step code, its own inputs
+        try:
+            rec["strong_cfg3"] = strong_cfg3(args, world, rank, dev, backend, base_of=A)
+        except Exception as e:  # noqa: BLE001 -- the headline line stands on its own
+            rec["strong_cfg3"] = {"error": f"{type(e).__name__}: {str(e)[:200]}"}
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         rec["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds, args.cpu_images, train)
         rec["cpu_baseline"]["gpu_over_cpu"] = rec["value"] / rec["cpu_baseline"]["value"]
