@@ -1320,7 +1320,10 @@ __global__ __launch_bounds__(1024) void roi_pool_bwd_lead_kernel(
     const int PHW = PH * PW;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int b = blockIdx.y;
+    // wave w of workgroup (x, y) takes image (y + w) mod N: every CU carries a mix of
+    // the images, whose flagged-RoI gathers differ (the kernel is issue-bound; round 6:
+    // 77.2-78.1 vs 78.5-79.3 µs op, span max 71.6 vs 74.3), each (image, channel) once
+    const int b = static_cast<int>((blockIdx.y + static_cast<unsigned>(wid)) % gridDim.y);
     const int c = blockIdx.x * CPW + wid;
     if (c >= C) return;  // whole wave; no workgroup barrier below
 #ifdef FRCNN_BWD_PROF
