@@ -54,7 +54,9 @@ def main():
             w = buf[gw].astype(np.float64)
             t0 = w[:, 4].min()
             st, en = (w[:, 4] - t0) / 100.0, (w[:, 5] - t0) / 100.0  # us
-            img = gw // (C * K)
+            # gw = (y * gridDim.x + x) * CPW + w, CPW = 16 at cfg5; wave w of workgroup row y
+            # owns image (y + w) mod N (images mixed within a workgroup)
+            img = (gw // (C * K) + gw % 16) % N
             span = en - st
             slow = np.argsort(span)[-32:]
             nfl = np.maximum(w[:, 6], 1)
