@@ -709,14 +709,14 @@ def train_step_fn(args, c, sets, base, first_image, ev):
             # retires between two samplers (~4-6 us each, profiles/r4_experiments.md):
             # one wait (prop_ready follows prep_ready on the same stream) and one
             # timing record per step
-            if args.rng_waits == "front":  # both samplers back to back (the prepares run ahead)
+            if args.rng_waits == "front":  # both creators' draws as one pass (the prepares run ahead)
                 s_rng.wait_event(prop_ready)
+                s_cnt = targets.target_draws(plan, pplan, rng, count=pt_out[j][3])
             else:
                 s_rng.wait_event(prep_ready[j])
-            targets.anchor_targets_draw(plan, rng=rng)
-            if args.rng_waits != "front":
+                targets.anchor_targets_draw(plan, rng=rng)
                 s_rng.wait_event(prop_ready)
-            s_cnt = targets.proposal_targets_draw(pplan, rng=rng, count=pt_out[j][3])
+                s_cnt = targets.proposal_targets_draw(pplan, rng=rng, count=pt_out[j][3])
             pt_drawn = torch.cuda.Event(enable_timing=timed)
             pt_drawn.record(s_rng)
             if timed:
@@ -910,17 +910,19 @@ def main():
                  "event_interval_us_in_pipeline": ev_ms * 1e3}
     if train:
         # the training step's critical path is not an HBM kernel: the target
-        # creators' draws walk numpy's sequential MT19937 stream, one workgroup
-        # each (at_sample_kernel, then pt_sample_kernel) on the draws' stream
-        dr = ev["draw"]  # the draws' stream period: one record per step after the second sampler
+        # creators' draws on numpy's sequential MT19937 stream, one chip-wide pass
+        # for both creators (frcnn_target_draws: draw_setup / _table / _group /
+        # _chain / _record kernels) on the draws' stream
+        dr = ev["draw"]  # the draws' stream period: one record per step after the draws
         gaps = [a.elapsed_time(b) for a, b in zip(dr[:-1], dr[1:])]
         draw_us = float(np.mean(gaps)) * 1e3 if gaps else None  # (--steps 1: no period)
         pool_roof["fwd_event_interval_us_in_pipeline"] = fwd_ms * 1e3
-        roof = {"bound": "latency", "kernel": "at_sample_kernel", "unit": "us/step",
-                "achieved": draw_us, "peak": None, "frac": None, "traffic": None,
-                "basis": "the draws' stream period (at_sample_kernel + pt_sample_kernel, one 1024-thread "
-                         "workgroup each, sequential MT19937 stream, + the stream's wait / record packets) "
-                         "between consecutive steps, HIP events; latency-bound, so no HBM / MFMA peak applies",
+        roof = {"bound": "latency", "kernel": "draw_setup_kernel + draw_table_kernel (chip-wide draws)",
+                "unit": "us/step", "achieved": draw_us, "peak": None, "frac": None, "traffic": None,
+                "basis": "the draws' stream period (both target creators' draws as one chip-wide pass: the MT19937 "
+                         "state blocks twisted on one CU, per-segment step-count tables over the chip, their "
+                         "chain, the recorded swaps; + the stream's wait / record packets) between consecutive "
+                         "steps, HIP events; latency-bound, so no HBM / MFMA peak applies",
                 "draws_share_of_step": None if draw_us is None else draw_us / (ms_step * 1e3),
                 "roi_pool_bwd": pool_roof}
         pool_roof = roof

@@ -63,8 +63,13 @@ int frcnn_probe_hw_ids(uint32_t* out, int nblocks, int spin, void* stream);
  *   "roi_pool_cg"    : "auto" | "4" | "8" | "16" (channels per RoIPool forward workgroup)
  *   "roi_pool_fwd_store": "auto" = "temporal" | "nt" (the wave forward's output stores
  *                      non-temporal: better beside concurrent kernels at cfg2, worse alone)
- *   "sampler"        : "auto" | "walk" (one workgroup walks the MT19937 stream: the target
- *                      creators' _draw / _sample entry points)
+ *   "sampler"        : "auto" = "chip" (the stream cut into 1024-word segments, each one's
+ *                      map of entering to leaving step count tabulated chip-wide and
+ *                      chained; the walk below runs instead when a step count leaves
+ *                      its planned range, or for > 128 images) | "walk" (one workgroup
+ *                      walks the MT19937 stream) | "chip_only" (no walk behind it) |
+ *                      "chip_tight" (zero-margin ranges: exercises the walk behind it);
+ *                      the target creators' _draw / _sample entry points
  * All paths give bit-identical results.  Not thread-safe against calls in
  * flight on other threads; set it before launching. */
 int frcnn_set_path(const char* op, const char* path);
@@ -192,8 +197,8 @@ int frcnn_roi_pool_bwd(const float* grad, const float* rois, const int32_t* argm
                        int N, int C, int H, int W, int PH, int PW, float spatial_scale,
                        float* grad_in, void* workspace, size_t ws_bytes, void* stream);
 /* The RoIPool backward kernel frcnn_roi_pool_bwd launches for this shape under
- * the current frcnn_set_path choice (e.g. "roi_pool_bwd_lead_kernel<6, 7>"),
- * NUL-terminated in name[len] (bench.py's label for it; the fused prep + lists
+ * the current frcnn_set_path choice (e.g. "roi_pool_bwd_lead_kernel<4, 7, 7>"),
+ * NUL-terminated in name[len] (bench.py's label for it; the per-image lists
  * launch before it is not named). */
 int frcnn_roi_pool_bwd_kernel(int64_t R, int N, int C, int H, int W, int PH, int PW, char* name, size_t len);
 
@@ -250,6 +255,13 @@ int frcnn_anchor_target_draw(int N, int A, int G, int n_sample, double pos_ratio
 int frcnn_anchor_target_finish(int N, int A, int G, const float* anchors, double* reg, int32_t* label,
                                int32_t* argmax, double* max_iou, void* workspace, size_t ws_bytes,
                                void* stream);
+/* The chip-wide draws' plan of the last _draw on this workspace (synchronous; a
+ * diagnostic, no reference counterpart): out[9] = fail (0: the segment tables held;
+ * 1: plan over the workspace's capacity; 2: a step count left its planned range --
+ * the walk did the draws), calls with >= 1 step, steps, segments, groups, state
+ * blocks, start pos, widest range, missed group (-1).  Returns 1 when the
+ * workspace has no chip-wide part (> 128 images: the walk only). */
+int frcnn_anchor_target_draw_status(int N, int A, int G, const void* workspace, size_t ws_bytes, int* out);
 
 /* utils/utils.py:207-276 ProposalTargetCreator.__call__, batched over N images in
  * the order of train.py:91-104.
@@ -291,6 +303,18 @@ int frcnn_proposal_target_finish(int N, int Rp, int G, int n_sample, const doubl
                                  const double* reg_std, const int32_t* sample_count, double* sample_roi,
                                  double* gt_roi_reg, double* gt_roi_label, void* workspace, size_t ws_bytes,
                                  void* stream);
+/* frcnn_anchor_target_draw then frcnn_proposal_target_draw on one RNG stream, as
+ * one pass (the order of train.py:71 / :91: every AnchorTarget draw, then every
+ * ProposalTarget draw, for the same N images): both prepares must have run on
+ * their workspaces (same arguments as the two _draw calls; the pass uses the
+ * anchor workspace's chip-wide part, frcnn_anchor_target_draw_status reads it).
+ * Bit-identical to the two calls in sequence. */
+int frcnn_target_draws(int N, int A, int G_at, int n_sample_at, double pos_ratio_at, void* at_workspace,
+                       size_t at_bytes, int Rp, int G_pt, int n_sample_pt, double pos_ratio_pt, void* pt_workspace,
+                       size_t pt_bytes, int32_t* sample_count, uint32_t* rng_state, void* stream);
+/* As frcnn_anchor_target_draw_status, for the last frcnn_proposal_target_draw. */
+int frcnn_proposal_target_draw_status(int N, int Rp, int G, int n_sample, const void* workspace, size_t ws_bytes,
+                                      int* out);
 
 #ifdef __cplusplus
 }

@@ -80,6 +80,9 @@ SIGNATURES = {
     "frcnn_proposal_target_finish": (I32, [I32, I32, I32, I32, P, P, P, P, P, P, P, SZ, P]),
     "frcnn_proposal_target_prepare": (I32, [I32, I32, P, P, I32, P, P, I32, F64, F64, F64, P, SZ, P]),
     "frcnn_proposal_target_sample": (I32, [I32, I32, I32, I32, F64, P, P, P, P, P, P, P, P, SZ, P]),
+    "frcnn_anchor_target_draw_status": (I32, [I32, I32, I32, P, SZ, P]),
+    "frcnn_proposal_target_draw_status": (I32, [I32, I32, I32, I32, P, SZ, P]),
+    "frcnn_target_draws": (I32, [I32, I32, I32, I32, F64, P, SZ, I32, I32, I32, F64, P, SZ, P, P, P]),
 }
 
 # diagnostic entry points of instrumented builds only (not in include/frcnn_capi.h)

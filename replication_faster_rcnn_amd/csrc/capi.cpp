@@ -81,8 +81,13 @@ extern "C" int frcnn_set_path(const char* op, const char* path) {
                                                               : kPathWide;
     } else if (is(op, "roi_pool_fwd_store") && (aut || is(path, "temporal") || is(path, "nt"))) {
         g_path.roi_store = is(path, "nt") ? 1 : 0;
-    } else if (is(op, "sampler") && (aut || is(path, "walk"))) {
-        g_path.sampler = aut ? kPathAuto : kPathWalk;
+    } else if (is(op, "sampler") && (aut || is(path, "walk") || is(path, "chip") || is(path, "chip_only") ||
+                                     is(path, "chip_tight"))) {
+        g_path.sampler = aut                   ? kPathAuto
+                         : is(path, "walk")      ? kPathWalk
+                         : is(path, "chip")      ? kPathChip
+                         : is(path, "chip_only") ? kPathChipOnly
+                                                 : kPathChipTight;
     } else if (is(op, "roi_pool_split")) {
         char* end = nullptr;
         const long v = aut ? 0 : std::strtol(path, &end, 10);

@@ -24,7 +24,10 @@ constexpr int kPathRing = 2;     // roi_pool_bwd: the RoI-at-a-time ring kernel 
 constexpr int kPathHybrid = 1;   // propose: fused per image + chip-wide first-chunk mask
 constexpr int kPathLazy = 2;     // propose: fused per image, lazy NMS from the first chunk on
 constexpr int kPathWide = 3;     // propose: chip-wide sort + bitmask NMS
-constexpr int kPathWalk = 1;     // sampler: one workgroup walks the MT19937 stream (auto)
+constexpr int kPathWalk = 1;       // sampler: one workgroup walks the MT19937 stream
+constexpr int kPathChip = 2;       // sampler: chip-wide segment tables, the walk as fallback (auto)
+constexpr int kPathChipOnly = 3;   // sampler: chip-wide, no fallback launched (tests)
+constexpr int kPathChipTight = 4;  // sampler: chip-wide with zero-margin domains (tests the fallback)
 struct PathCfg {
     int roi_fwd = kPathAuto;
     int roi_bwd = kPathAuto;

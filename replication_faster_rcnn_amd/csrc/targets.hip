@@ -21,6 +21,7 @@
 //    the recorded swaps (fy_final): the last m positions for AnchorTarget
 //    (which m elements survive the disable), the first k for ProposalTarget
 //    (in order).
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 
@@ -720,9 +721,11 @@ __device__ void fy_final(int cnt, int rec_lo, int p_lo, int p_hi, const int* J, 
 __global__ __launch_bounds__(kSampThreads) void at_sample_kernel(
     int N, int A, int n_sample, int n_pos_max, const int* __restrict__ pos_list,
     const int* __restrict__ neg_list, const int* __restrict__ npos, const int* __restrict__ nneg,
-    uint32_t* __restrict__ rng, int* __restrict__ sampled, int4* __restrict__ calls, int* __restrict__ jrec) {
+    uint32_t* __restrict__ rng, int* __restrict__ sampled, int4* __restrict__ calls, int* __restrict__ jrec,
+    const int* __restrict__ gate) {
     __shared__ WalkLds S;
     __shared__ int J[kMaxKeep];
+    if (gate && *gate == 0) return;  // the chip-wide draws succeeded (draw_chain_kernel)
     SPROF_T0();
     Stream st;
     stream_load(S, st, rng);
@@ -879,9 +882,10 @@ __global__ __launch_bounds__(kSampThreads) void pt_sample_kernel(
     int N, int stride, int n_sample, int pos_per_image, const int* __restrict__ pos_list,
     const int* __restrict__ neg_list, const int* __restrict__ npos, const int* __restrict__ nneg,
     uint32_t* __restrict__ rng, int* __restrict__ scount,
-    int* __restrict__ spos, int4* __restrict__ calls, int* __restrict__ jrec) {
+    int* __restrict__ spos, int4* __restrict__ calls, int* __restrict__ jrec, const int* __restrict__ gate) {
     __shared__ WalkLds S;
     __shared__ int J[kMaxKeep];
+    if (gate && *gate == 0) return;  // the chip-wide draws succeeded (draw_chain_kernel)
     Stream st;
     stream_load(S, st, rng);
     __syncthreads();
@@ -939,6 +943,740 @@ __global__ __launch_bounds__(kSampThreads) void samp_emit_kernel(const int4* __r
     } else {
         int* out = sample + static_cast<size_t>(n) * n_sample + c.w;
         fy_final(cnt, rlo, 0, c.z, Jl, FL, [&](int p, int v) { out[p] = lst[v]; });
+    }
+}
+
+// ========================================================= chip-wide draws
+// The draws of at_sample_kernel / pt_sample_kernel (one MT19937 stream, every
+// choice() call of every image in order), spread over the chip.  The walk's
+// state between words is (q, K): q words consumed, K steps accepted; the
+// calls' bounds are a function of K alone (walk c runs bounds hi_c .. 1 while
+// K is in [cum[c] - hi_c, cum[c])), so a stretch of words maps each entering K
+// to a leaving K.  The stream is cut into segments of seg_l words (1024, or 256 for short streams) and, for
+// every segment, that map is tabulated over the K's the walk can plausibly
+// hold at the segment's start -- the domain: the expected K from the calls'
+// mask regions (E[words per step] = (mask + 1) / (bound + 1)) +- mult sigma --
+// one lane per entering K (draw_table_kernel, chip-wide; a lane's walk is three
+// VALU per word, the mask and the call refreshed only at the wave's nearest
+// region or call edge).  Tables are composed over groups of kGrpG segments
+// (draw_group_kernel) and chained over the groups (draw_chain_kernel): the
+// exact K at every segment start.  Segments holding a recorded swap or the
+// stream's last draw are then walked exactly, one wave each
+// (draw_record_kernel).  A K outside a domain or a plan over the workspace's
+// capacity sets hdr.fail and the serial sampler, gated on it, does the draws:
+// exact either way (the words, bounds and acceptance rule are the serial
+// walk's; only the order of evaluation differs).
+constexpr int kSegLMax = 1024;       // words per segment: 1024, or 256 for short streams
+constexpr int kGrpG = 16;            // segments per group
+constexpr int kDrawWalks = 256;      // calls with >= 1 step (N <= 128 images)
+constexpr int kDrawDcap = 4096;      // entering K's per segment
+constexpr int kDrawSegMax = 1024;    // segments (1 M words)
+constexpr int kDrawHiMax = 65535;    // bounds < 2^16: <= 16 mask regions per call
+constexpr int kDrawPieces = kDrawWalks * 16;
+constexpr int kChainLds = 65536;     // composite entries draw_chain_kernel stages in LDS
+constexpr uint16_t kMiss = 0xffffu;  // a leaving K outside the next segment's domain
+static_assert(kGrpG * kDrawDcap * 2 <= 128 * 1024, "a group's tables fit draw_group_kernel's LDS");
+static_assert(kDrawSegMax <= 1024 && 2 * kDrawWalks / 2 <= 1024, "one thread per segment / call in the setup");
+
+struct DrawHdr {
+    int fail;  // 0: the chip-wide draws hold; 1: plan over capacity; 2: a K left its domain
+    int nw, ktot, nseg, ngrp, nblk, off0, dmax;
+    int miss;   // the group whose composite missed (fail 2), else -1
+    int seg_l;  // words per segment
+};
+
+struct DrawCap {
+    int smax, nbmax, tabmax, premax;  // smax == 0: the serial sampler only
+};
+
+struct DrawBufs {
+    DrawHdr* hdr;
+    int* w_hi;    // [kDrawWalks] walk c: bounds hi_c .. 1
+    int* w_cum;   // [kDrawWalks] K after walk c
+    int* w_rec;   // [kDrawWalks] lowest recorded bound
+    int* w_row;   // [kDrawWalks] jrec row (the choice() call)
+    int* s_lo;    // [smax + 1] segment s's domain: entering K in [s_lo, s_lo + s_d)
+    int* s_d;     // [smax + 1]
+    int* s_toff;  // [smax + 1] table offsets (prefix of s_d)
+    int* s_item;  // [smax + 1] prefix of ceil(s_d / 256): a workgroup per 256 entering K's
+    int* g_poff;  // [smax / kGrpG + 2] group prefix-table offsets
+    int* kseg;    // [smax + 1] exact K at each segment start
+    uint16_t* tab;  // per segment, per entering K: leaving K - s_lo[s + 1] (kMiss outside)
+    uint16_t* pre;  // per group, per segment j, per entering K of the group: K after j (rel.)
+    uint32_t* raw;  // [nbmax][624] state blocks (block 0 = the key handed in)
+    uint32_t* tw;   // the words tempered, from the draws' first: word q of the draws is tw[q]
+};
+
+template <class T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const T u = __shfl_up(v, d, 64);
+        if (lane >= d) v += u;
+    }
+    return v;
+}
+// Inclusive scan of one value per thread over a 1024-thread block (sh: 16 slots).
+template <class T>
+__device__ T block_incl_scan(T v, T* sh, T& tot) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    v = wave_incl_scan(v);
+    if (lane == 63) sh[wid] = v;
+    __syncthreads();
+    T pre = 0, all = 0;
+    for (int i = 0; i < 16; ++i) {
+        const T x = sh[i];
+        if (i < wid) pre += x;
+        all += x;
+    }
+    __syncthreads();
+    tot = all;
+    return v + pre;
+}
+
+// H(n) = sum 1/i and H2(n) = sum 1/i^2 (asymptotic past 32; the plan only
+// centres the domains, it decides nothing)
+struct HarmTab {
+    double h1[65], h2[65];
+};
+constexpr HarmTab make_harm() {
+    HarmTab t{};
+    double a = 0.0, b = 0.0;
+    for (int i = 1; i <= 64; ++i) {
+        a += 1.0 / i;
+        b += 1.0 / (static_cast<double>(i) * i);
+        t.h1[i] = a;
+        t.h2[i] = b;
+    }
+    return t;
+}
+__constant__ HarmTab kHarm = make_harm();
+__device__ double harm1(int n) {
+    if (n <= 64) return kHarm.h1[n];
+    const double x = n;
+    return log(x) + 0.57721566490153286 + 0.5 / x - 1.0 / (12.0 * x * x);
+}
+__device__ double harm2(int n) {
+    if (n <= 64) return kHarm.h2[n];
+    const double x = n + 1.0;  // pi^2 / 6 - trigamma(n + 1)
+    return 1.6449340668482264 - (1.0 / x + 0.5 / (x * x) + 1.0 / (6.0 * x * x * x));
+}
+
+struct DrawSetupLds {
+    double cE[kDrawPieces + 1];  // expected words before piece p (walk-major, regions high to low)
+    double cV[kDrawPieces + 1];  // their variance
+    int cum[kDrawWalks], hi[kDrawWalks];
+    int sd[kDrawSegMax + 1];
+    uint32_t blk[8][kMtN];  // the twist's LDS ring
+    double shd[16];
+    int shi[16];
+    int nw, ktot, fail;
+};
+
+// One workgroup: the call list (kOp 0: AnchorTarget's two calls per image,
+// utils/utils.py:190-202; 1: ProposalTarget's, :248-258) with the outputs that
+// need no RNG, the segment plan, and the state blocks the segments read.
+// The calls one chip-wide pass draws, in stream order: AnchorTarget's two per
+// image (utils/utils.py:190-202), then ProposalTarget's (:248-258) -- train.py:71
+// and :91 make every AnchorTarget draw before any ProposalTarget one, so both
+// creators' calls can share one pass (n_at or n_pt may be 0).
+struct DrawOps {
+    int n_at, at_n_sample, at_pos_max;
+    const int* at_npos;
+    const int* at_nneg;
+    int* at_sampled;
+    int4* at_calls;
+    int* at_jrec;
+    int n_pt, pt_n_sample, pt_pos_per_image;
+    const int* pt_npos;
+    const int* pt_nneg;
+    int4* pt_calls;
+    int* pt_scount;
+    int* pt_spos;
+    int* pt_jrec;
+};
+
+// One workgroup: the call list with the outputs that need no RNG, the segment
+// plan, and the state blocks the segments read.
+__global__ __launch_bounds__(1024) void draw_setup_kernel(DrawOps ops, const uint32_t* __restrict__ rng, DrawCap cap,
+                                                          float mult, int slack, DrawBufs B) {
+    __shared__ DrawSetupLds L;
+    const int tid = threadIdx.x;
+    // ---- calls (thread = call; its jrec row is its index)
+    int steps = 0, isw = 0, rec = 0;
+    const int na = 2 * ops.n_at;
+    if (tid < na) {
+        const int n = tid >> 1, call = tid & 1;
+        const int P = ops.at_npos[n], Q = ops.at_nneg[n];
+        const int cnt = call ? Q : P;
+        const int n_pos_max = ops.at_pos_max;
+        const int pos_after = P > n_pos_max ? n_pos_max : P;
+        const int m = call ? ops.at_n_sample - pos_after : n_pos_max;  // survivors
+        const bool do_call = cnt > m;
+        ops.at_sampled[tid] = do_call ? 1 : 0;
+        ops.at_calls[tid] = do_call ? make_int4(cnt, cnt - m, cnt, 0) : make_int4(0, 0, 0, 0);
+        if (do_call && cnt >= 2) {
+            isw = 1;
+            steps = cnt - 1;
+            rec = cnt - m;
+        }
+    } else if (tid < na + 2 * ops.n_pt) {
+        const int i = tid - na, n = i >> 1, call = i & 1;
+        const int P = ops.pt_npos[n], Q = ops.pt_nneg[n];
+        const int cnt = call ? Q : P;
+        const int kp = P < ops.pt_pos_per_image ? P : ops.pt_pos_per_image;
+        int kn = ops.pt_n_sample - kp;
+        kn = Q < kn ? Q : kn;
+        ops.pt_calls[i] = cnt > 0 ? make_int4(cnt, 1, call ? kn : kp, call ? kp : 0) : make_int4(0, 0, 0, 0);
+        if (call == 0) {
+            ops.pt_scount[n] = kp + kn;
+            ops.pt_spos[n] = kp;
+        }
+        if (cnt >= 2) {
+            isw = 1;
+            steps = cnt - 1;
+            rec = 1;
+        }
+    }
+    if (tid == 0) L.fail = 0;
+    int nw = 0, ktot = 0;
+    const int wi = block_incl_scan(isw, L.shi, nw);
+    const int ki = block_incl_scan(steps, L.shi, ktot);
+    if (isw) {
+        const int c = wi - 1;
+        L.cum[c] = ki;
+        L.hi[c] = steps;
+        B.w_hi[c] = steps;
+        B.w_cum[c] = ki;
+        B.w_rec[c] = rec;
+        B.w_row[c] = tid;
+        if (steps > kDrawHiMax) L.fail = 1;
+    }
+    __syncthreads();
+    // ---- expected words / variance per (walk, mask region), in stream order
+    const int P = nw * 16;
+    double e4[4], v4[4], es = 0.0, vs = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int p = tid * 4 + r;
+        double E = 0.0, V = 0.0;
+        if (p < P) {
+            const int c = p >> 4, j = 15 - (p & 15);
+            const int hic = L.hi[c], bl = 1 << j;
+            if (bl <= hic) {
+                const int bh = min((2 << j) - 1, hic);
+                const double M = static_cast<double>(2 << j);
+                E = M * (harm1(bh + 1) - harm1(bl));
+                V = M * M * (harm2(bh + 1) - harm2(bl)) - E;
+            }
+        }
+        e4[r] = E;
+        v4[r] = V;
+        es += E;
+        vs += V;
+    }
+    double Etot = 0.0, Vtot = 0.0;
+    double ea = block_incl_scan(es, L.shd, Etot) - es;
+    double va = block_incl_scan(vs, L.shd, Vtot) - vs;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int p = tid * 4 + r;
+        if (p < P) {
+            L.cE[p] = ea;
+            L.cV[p] = va;
+        }
+        ea += e4[r];
+        va += v4[r];
+    }
+    if (tid == 0) {
+        L.cE[P] = Etot;
+        L.cV[P] = Vtot;
+    }
+    __syncthreads();
+    // ---- segments: domain of the K at each segment start
+    const int off0 = static_cast<int>(rng[kMtN]);
+    int S = 0, SL = kSegLMax;
+    if (ktot > 0) {  // short streams (ProposalTarget's) in 256-word segments: shorter lane walks
+        const double span = Etot + mult * sqrt(Vtot) + slack + 64.0;
+        S = static_cast<int>(ceil(span / 256.0));
+        if (S <= 256) SL = 256;
+        else S = static_cast<int>(ceil(span / kSegLMax));
+    }
+    if (S > cap.smax) {
+        if (tid == 0) L.fail = 1;
+        S = 0;
+    }
+    int D = 0, lo = 0;
+    if (tid <= S && S > 0) {
+        const int s = tid;
+        if (s == 0) {
+            lo = 0;
+            D = 1;
+        } else if (s == S) {
+            lo = ktot;
+            D = 1;
+        } else {
+            // the expected K at word x (the calls' mask regions, E[words per step]
+            // = M / (b + 1) inverted with H(n) ~ ln(n + 1/2) + gamma) and the
+            // variance of the words spent reaching it
+            auto khat = [&](double x, double& var) -> double {
+                if (x <= 0.0) {
+                    var = 0.0;
+                    return 0.0;
+                }
+                int a = 0, z = P;  // largest p with cE[p] <= x
+                while (a < z) {
+                    const int m = (a + z + 1) >> 1;
+                    if (L.cE[m] <= x) a = m;
+                    else z = m - 1;
+                }
+                if (a >= P) {
+                    var = Vtot;
+                    return static_cast<double>(ktot);
+                }
+                const int c = a >> 4, j = 15 - (a & 15);
+                const int hic = L.hi[c];
+                const int bl = 1 << j, bh = min((2 << j) - 1, hic);
+                const double M = static_cast<double>(2 << j);
+                const int K0 = L.cum[c] - hic + (hic - bh);
+                double bf = (bh + 1.5) * exp(-(x - L.cE[a]) / M) - 1.5;
+                bf = fmin(fmax(bf, bl - 1.0), static_cast<double>(bh));
+                const double Vp = L.cV[a + 1] - L.cV[a];
+                var = fmax(L.cV[a] + Vp * (bh - bf) / (bh - bl + 1.0), 0.0);
+                return K0 + (bh - bf);
+            };
+            // the domain in WORD space: the walk's words to reach a K deviate from
+            // the expectation like a Gaussian path (sigma_W), and K is read off the
+            // expectation at q -+ mult sigma_W -- across mask-region edges too, where
+            // the acceptance rate jumps (a linearised sigma_K under-covers there)
+            const double q = static_cast<double>(s) * SL;
+            double var = 0.0, vd = 0.0;
+            const double kq = khat(q, var);
+            const double sw = mult * sqrt(var);
+            lo = max(0, static_cast<int>(floor(khat(q - sw, vd))) - slack);
+            int hi = min(ktot, static_cast<int>(ceil(khat(q + sw, vd))) + slack);
+            if (hi - lo + 1 > kDrawDcap) {  // narrower: only a miss more likely
+                const int kc = static_cast<int>(floor(kq + 0.5));
+                lo = max(0, min(kc - kDrawDcap / 2, ktot - kDrawDcap + 1));
+                hi = min(ktot, lo + kDrawDcap - 1);
+            }
+            D = hi - lo + 1;
+        }
+        B.s_lo[s] = lo;
+        B.s_d[s] = D;
+        L.sd[s] = D;
+    }
+    // table offsets and wave items over segments 0 .. S-1
+    const int dt = tid < S ? D : 0;
+    int tabn = 0, itn = 0;
+    const int ti = block_incl_scan(dt, L.shi, tabn);
+    const int ii = block_incl_scan((dt + 255) >> 8, L.shi, itn);
+    if (tid < S) {
+        B.s_toff[tid] = ti - dt;
+        B.s_item[tid] = ii - ((dt + 255) >> 8);
+    }
+    if (tid == 0) {
+        B.s_toff[S] = tabn;
+        B.s_item[S] = itn;
+    }
+    __syncthreads();  // L.sd
+    const int ngrp = (S + kGrpG - 1) / kGrpG;
+    int pg = 0, cg = 0;
+    if (tid < ngrp) {
+        const int gs = min(kGrpG, S - tid * kGrpG);
+        pg = gs * L.sd[tid * kGrpG];
+        cg = L.sd[tid * kGrpG];
+    }
+    int pren = 0, chn = 0;
+    const int pi = block_incl_scan(pg, L.shi, pren);
+    (void)block_incl_scan(cg, L.shi, chn);
+    int dmx = 0;
+    {
+        int dm = tid < S ? D : 0;
+        const int dw = static_cast<int>(__ockl_wfred_max_u32(static_cast<uint32_t>(dm)));
+        if ((tid & 63) == 0) L.shi[tid >> 6] = dw;
+        __syncthreads();
+        for (int i = 0; i < 16; ++i) dmx = max(dmx, L.shi[i]);
+        __syncthreads();
+    }
+    if (tid < ngrp) B.g_poff[tid] = pi - pg;
+    const int nblk = S > 0 ? (off0 + S * SL - 1) / kMtN + 1 : 0;
+    if (tid == 0) {
+        B.g_poff[ngrp] = pren;
+        if (tabn > cap.tabmax || pren > cap.premax || chn > kChainLds || nblk > cap.nbmax) L.fail = 1;
+    }
+    __syncthreads();
+    const int fail = L.fail;
+    if (tid == 0) {
+        DrawHdr h;
+        h.fail = fail;
+        h.nw = nw;
+        h.ktot = ktot;
+        h.nseg = fail ? 0 : S;
+        h.ngrp = fail ? 0 : ngrp;
+        h.nblk = nblk;
+        h.off0 = off0;
+        h.dmax = dmx;
+        h.miss = -1;
+        h.seg_l = SL;
+        *B.hdr = h;
+    }
+    if (fail || nblk == 0) return;  // (block-uniform)
+    // ---- the state blocks the segments read: block 0 is the key handed in.
+    // Waves 0-3 twist block b from block b - 1 in an LDS ring of kTwRing blocks
+    // (read, mix, write: the only work between two barriers); waves 4-15 copy
+    // block b - 1 out (raw, and tempered from the draws' first word on) meanwhile.
+    constexpr int kTwRing = 8;
+    for (int i = tid; i < kMtN; i += 1024) L.blk[0][i] = rng[i];
+    __syncthreads();
+    for (int b = 1; b <= nblk; ++b) {
+        if (tid < 256) {
+            const int t = tid;
+            if (b < nblk && t < kMtN - kMtM) {  // as mt_twist: words t, t + 227, t + 454
+                const uint32_t* old = L.blk[(b - 1) % kTwRing];
+                uint32_t* nw_ = L.blk[b % kTwRing];
+                // every LDS read first (clamped indices): one round trip per block
+                const uint32_t o0 = old[t], o1 = old[t + 1], o397 = old[t + kMtM];
+                const uint32_t o227 = old[t + 227], o228 = old[t + 228];
+                const uint32_t o454 = old[min(t + 454, kMtN - 1)], o455 = old[min(t + 455, kMtN - 1)];
+                const uint32_t z0 = old[0], z1 = old[1], z397 = old[kMtM];
+                const uint32_t a = o397 ^ mt_mix(o0, o1);
+                const uint32_t bb = a ^ mt_mix(o227, o228);
+                nw_[t] = a;
+                nw_[t + 227] = bb;
+                if (t + 454 <= kMtN - 1) {
+                    // word 623 wraps to the new word 0 (recomputed here)
+                    const uint32_t hi_in = t + 454 < kMtN - 1 ? o455 : (z397 ^ mt_mix(z0, z1));
+                    nw_[t + 454] = bb ^ mt_mix(o454, hi_in);
+                }
+            }
+        } else {  // copy block b - 1 out
+            const uint32_t* src = L.blk[(b - 1) % kTwRing];
+            uint32_t* rg = B.raw + static_cast<size_t>(b - 1) * kMtN;
+            const int a0 = (b - 1) * kMtN - off0;  // tw index of the block's word 0
+            for (int i = tid - 256; i < kMtN; i += 768) {
+                const uint32_t v = src[i];
+                rg[i] = v;
+                if (a0 + i >= 0) B.tw[a0 + i] = mt_temper(v);
+            }
+        }
+        // LDS-only barrier: the copies' global stores need not land before the next
+        // twist (__syncthreads would wait for them)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+}
+
+// One workgroup per 256 entering K's of a segment (a wave per 64): the
+// segment's words staged in LDS, each lane walks them from its own K.  Per
+// word: v = w & mask, accept iff v < bound + 1, bound -= accepted (3 VALU, the
+// word a broadcast LDS read per four); the masks and the walks' ends are
+// refreshed only after `rem` words, the wave's least distance (in acceptances)
+// to a lane's region edge or walk end.
+__global__ __launch_bounds__(256) void draw_table_kernel(const DrawHdr* __restrict__ hdr, DrawBufs B) {
+    __shared__ int cum[kDrawWalks + 1];
+    __shared__ int his[kDrawWalks + 1];
+    __shared__ int item[kDrawSegMax + 1];
+    __shared__ uint4 words[kSegLMax / 4];
+    if (hdr->fail) return;
+    const int nw = hdr->nw, ktot = hdr->ktot, S = hdr->nseg, L = hdr->seg_l;
+    for (int i = threadIdx.x; i < nw; i += 256) {
+        cum[i] = B.w_cum[i];
+        his[i] = B.w_hi[i];
+    }
+    for (int i = threadIdx.x; i <= S; i += 256) item[i] = B.s_item[i];
+    if (threadIdx.x == 0) {
+        cum[nw] = 0x7fffffff;
+        his[nw] = 0;
+    }
+    __syncthreads();
+    const int nitems = item[S];
+    const int lane = threadIdx.x & 63;
+    for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+        int a = 0, z = S - 1;  // segment: largest s with item[s] <= it
+        while (a < z) {
+            const int m = (a + z + 1) >> 1;
+            if (item[m] <= it) a = m;
+            else z = m - 1;
+        }
+        const int s = __builtin_amdgcn_readfirstlane(a);
+        {
+            const uint4* src = reinterpret_cast<const uint4*>(B.tw + static_cast<size_t>(s) * L);
+            for (int i = threadIdx.x; i < L / 4; i += 256) words[i] = src[i];
+        }
+        __syncthreads();
+        const int k = (it - item[s]) * 256 + static_cast<int>(threadIdx.x);
+        const int D = B.s_d[s];
+        if (__builtin_amdgcn_readfirstlane(k - lane) < D) {  // (a wave past the domain skips)
+            const int Dn = B.s_d[s + 1];
+            const int lon = B.s_lo[s + 1];
+            const int K = B.s_lo[s] + k;
+            int c = 0;
+            {
+                int l = 0, r = nw;  // first walk with cum > K (nw: the draws are over)
+                while (l < r) {
+                    const int m = (l + r) >> 1;
+                    if (cum[m] > K) r = m;
+                    else l = m + 1;
+                }
+                c = l;
+            }
+            uint32_t bnd = c < nw ? static_cast<uint32_t>(cum[c] - K) + 1u : 0u;  // bound + 1; 0: done
+            uint32_t msk = 0;
+            int rem = 0;
+            uint4 wn[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) wn[u] = words[u];
+            for (int t0 = 0; t0 < L; t0 += 16) {
+                uint32_t w[16];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    w[4 * u] = wn[u].x;
+                    w[4 * u + 1] = wn[u].y;
+                    w[4 * u + 2] = wn[u].z;
+                    w[4 * u + 3] = wn[u].w;
+                }
+                const int tn = t0 + 16 < L ? t0 + 16 : t0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) wn[u] = words[tn / 4 + u];
+                if (rem >= 16) {  // no lane reaches a region edge or walk end
+                    // accepted iff (w & mask) < bound + 1, both < 2^17: the sign of their
+                    // difference, all in VGPRs (a compare would route every word's decision
+                    // through VCC, an SGPR round trip per word on the dependency chain)
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) bnd -= ((w[u] & msk) - bnd) >> 31;
+                    rem -= 16;
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 16; ++u) {
+                        if (rem == 0) {
+                            if (bnd == 1u) {  // walk c ended: the next call's first bound
+                                ++c;
+                                bnd = c < nw ? static_cast<uint32_t>(his[c]) + 1u : 0u;
+                            }
+                            const uint32_t b = bnd - 1u;
+                            msk = 0xffffffffu >> __builtin_clz(b | 1u);
+                            const uint32_t run = bnd ? b - (msk >> 1) : 0x7fffffffu;  // >= 1
+                            rem = static_cast<int>(__ockl_wfred_min_u32(run));
+                        }
+                        bnd -= ((w[u] & msk) - bnd) >> 31;
+                        --rem;
+                    }
+                }
+            }
+            if (k < D) {
+                const int Ko = c < nw ? cum[c] - static_cast<int>(bnd - 1u) : ktot;
+                const int rel = Ko - lon;
+                B.tab[B.s_toff[s] + k] = (rel >= 0 && rel < Dn) ? static_cast<uint16_t>(rel) : kMiss;
+            }
+        }
+        __syncthreads();  // the words are restaged next item
+    }
+}
+
+// One workgroup per group of kGrpG segments: its tables staged in LDS, each
+// entering K of the group's first segment followed through them; the K after
+// every segment is kept (pre), the last one is the group's composite.
+__global__ __launch_bounds__(1024) void draw_group_kernel(const DrawHdr* __restrict__ hdr, DrawBufs B) {
+    __shared__ uint16_t st[kGrpG * kDrawDcap];
+    __shared__ int soff[kGrpG + 1];
+    if (hdr->fail) return;
+    const int g = blockIdx.x;
+    const int S = hdr->nseg;
+    if (g >= hdr->ngrp) return;
+    const int s0 = g * kGrpG, gs = min(kGrpG, S - s0);
+    if (threadIdx.x <= gs) soff[threadIdx.x] = B.s_toff[s0 + threadIdx.x];
+    __syncthreads();
+    const int base = soff[0], n = soff[gs] - base;
+    for (int i = threadIdx.x; i < n; i += 1024) st[i] = B.tab[base + i];
+    __syncthreads();
+    const int D0 = B.s_d[s0];
+    uint16_t* pg = B.pre + B.g_poff[g];
+    for (int k = threadIdx.x; k < D0; k += 1024) {
+        uint32_t v = static_cast<uint32_t>(k);
+        for (int j = 0; j < gs; ++j) {
+            if (v != kMiss) v = st[soff[j] - base + v];
+            pg[static_cast<size_t>(j) * D0 + k] = static_cast<uint16_t>(v);
+        }
+    }
+}
+
+// One workgroup: the group composites staged in LDS and chained from K = 0
+// (one lane), then the exact K at every segment start from the groups'
+// prefix tables.  A miss anywhere on the path hands the draws to the serial
+// sampler (hdr.fail = 2).
+__global__ __launch_bounds__(1024) void draw_chain_kernel(DrawHdr* __restrict__ hdr, DrawBufs B) {
+    __shared__ uint16_t comp[kChainLds];
+    __shared__ int coff[kDrawSegMax / kGrpG + 2];
+    __shared__ int d0[kDrawSegMax / kGrpG + 2];
+    __shared__ int vg[kDrawSegMax / kGrpG + 2];
+    __shared__ int bad;
+    if (hdr->fail) return;
+    const int S = hdr->nseg, ngrp = hdr->ngrp;
+    if (S == 0) return;
+    const int tid = threadIdx.x;
+    if (tid < ngrp) d0[tid] = B.s_d[tid * kGrpG];
+    if (tid == 0) bad = 0;
+    __syncthreads();
+    if (tid == 0) {
+        int o = 0;
+        for (int g = 0; g < ngrp; ++g) {
+            coff[g] = o;
+            o += d0[g];
+        }
+        coff[ngrp] = o;
+    }
+    __syncthreads();
+    // every composite entry loaded at once (one memory latency, not one per group)
+    const int ntot = coff[ngrp];
+    for (int i = tid; i < ntot; i += 1024) {
+        int a = 0, z = ngrp - 1;  // group: largest g with coff[g] <= i
+        while (a < z) {
+            const int m = (a + z + 1) >> 1;
+            if (coff[m] <= i) a = m;
+            else z = m - 1;
+        }
+        const int gs = min(kGrpG, S - a * kGrpG);
+        comp[i] = B.pre[B.g_poff[a] + static_cast<size_t>(gs - 1) * d0[a] + (i - coff[a])];
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t v = 0;  // K = 0 at the stream start: entry 0 of segment 0's domain {0}
+        for (int g = 0; g < ngrp; ++g) {
+            vg[g] = static_cast<int>(v);
+            v = comp[coff[g] + v];
+            if (v == kMiss) {
+                bad = 1 + g;
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    if (bad) {
+        if (tid == 0) {
+            hdr->fail = 2;
+            hdr->miss = bad - 1;
+        }
+        return;
+    }
+    for (int s = tid; s <= S; s += 1024) {
+        int K = 0;
+        if (s > 0) {
+            const int g = (s - 1) / kGrpG, j = (s - 1) % kGrpG;
+            K = B.s_lo[s] + B.pre[B.g_poff[g] + static_cast<size_t>(j) * d0[g] + vg[g]];
+        }
+        B.kseg[s] = K;
+    }
+}
+
+// One wave per segment: the segment's words walked exactly from the K the
+// chain found, 64 at a time (ballot fixed point, as the serial walk's), when
+// the segment holds a recorded swap or the stream's last draw; the last draw's
+// segment hands the state back (numpy's pos = 1..624 within the key block).
+__global__ __launch_bounds__(64) void draw_record_kernel(const DrawHdr* __restrict__ hdr, DrawBufs B,
+                                                         DrawOps ops, uint32_t* __restrict__ rng) {
+    __shared__ int cum[kDrawWalks + 1];
+    __shared__ int rec[kDrawWalks];
+    __shared__ int row[kDrawWalks];
+    if (hdr->fail) return;
+    const int s = blockIdx.x;
+    const int S = hdr->nseg;
+    if (s >= S) return;
+    const int nw = hdr->nw, ktot = hdr->ktot, off0 = hdr->off0;
+    const int lane = threadIdx.x;
+    const int K0 = B.kseg[s], K1 = B.kseg[s + 1];
+    if (K0 == K1) return;  // no acceptance in this segment
+    for (int i = lane; i < nw; i += 64) {
+        cum[i] = B.w_cum[i];
+        rec[i] = B.w_rec[i];
+        row[i] = B.w_row[i];
+    }
+    if (lane == 0) cum[nw] = 0x7fffffff;
+    __syncthreads();
+    bool want = K1 == ktot;  // the stream's last acceptance is in here
+    for (int c = lane; c < nw; c += 64) {
+        const int hic = c ? cum[c] - cum[c - 1] : cum[0];
+        const int st = cum[c] - hic;  // K at the walk's first step (bound hic)
+        const int r1 = st + hic - rec[c];  // K at its lowest recorded bound
+        if (rec[c] <= hic && st < K1 && r1 >= K0) want = true;
+    }
+    if (!__builtin_amdgcn_ballot_w64(want)) return;
+    auto walk_of = [&](int K) {
+        int l = 0, r = nw;
+        while (l < r) {
+            const int m = (l + r) >> 1;
+            if (cum[m] > K) r = m;
+            else l = m + 1;
+        }
+        return l;
+    };
+    const int L = hdr->seg_l;
+    const uint32_t* wp = B.tw + static_cast<size_t>(s) * L;
+    uint32_t wv[kSegLMax / 64];  // every chunk's word loaded at once (one memory latency)
+#pragma unroll
+    for (int ch = 0; ch < kSegLMax / 64; ++ch) wv[ch] = ch * 64 < L ? wp[ch * 64 + lane] : 0u;
+    int Kc = K0, qend = -1;
+#pragma unroll
+    for (int ch = 0; ch < kSegLMax / 64; ++ch) {
+        if (ch * 64 >= L || Kc >= K1) break;
+        const uint32_t w = wv[ch];
+        const int c0 = walk_of(Kc);
+        const bool one = c0 < nw && Kc + 64 <= cum[c0];  // the chunk stays in walk c0
+        const uint32_t b0 = c0 < nw ? static_cast<uint32_t>(cum[c0] - Kc) : 0u;
+        const float pa = (static_cast<float>(b0) + 1.0f) / (static_cast<float>(mask_for(b0 | 1u)) + 1.0f);
+        uint64_t ac = 0;
+        int c = c0, K = Kc;
+        uint32_t b = 0;
+        bool acc = false;
+        int below = static_cast<int>(static_cast<float>(lane) * pa);
+        for (int itn = 0;; ++itn) {
+            K = Kc + below;
+            c = c0;  // the lane's walk: c0 or a few past it (the chunk accepts <= 64)
+            if (!one)
+                while (c < nw && cum[c] <= K) ++c;
+            b = (c < nw && K < ktot) ? static_cast<uint32_t>(cum[c] - K) : 0u;
+            acc = max(w & mask_nz(b), 1u) <= b;
+            const uint64_t nac = __builtin_amdgcn_ballot_w64(acc);
+            if (itn > 0 && nac == ac) break;
+            ac = nac;
+            below = static_cast<int>(__builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(ac >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(ac), 0u)));
+        }
+        if (acc) {
+            if (static_cast<int>(b) >= rec[c]) {
+                const int r = row[c], na = 2 * ops.n_at;
+                int* jrow = r < na ? ops.at_jrec + static_cast<size_t>(r) * kMaxKeep
+                                   : ops.pt_jrec + static_cast<size_t>(r - na) * kMaxKeep;
+                jrow[static_cast<int>(b) - rec[c]] = static_cast<int>(w & mask_nz(b));
+            }
+            if (K + 1 == ktot) qend = s * L + ch * 64 + lane + 1;
+        }
+        Kc += __popcll(ac);
+    }
+    const int qe = static_cast<int>(__ockl_wfred_max_i32(qend));
+    if (qe > 0) {
+        const int A = off0 + qe;  // words [off0, A) consumed: the key is block (A-1)/624
+        const int blk = (A - 1) / kMtN;
+        const uint32_t* src = B.raw + static_cast<size_t>(blk) * kMtN;
+        for (int i = lane; i < kMtN; i += 64) rng[i] = src[i];
+        if (lane == 0) rng[kMtN] = static_cast<uint32_t>((A - 1) % kMtN + 1);
+    }
+}
+
+// "chip_only" (tests): when the plan failed nothing was drawn, so the finishing
+// kernels get no calls and no samples rather than stale swap records.
+__global__ __launch_bounds__(256) void draw_poison_kernel(const DrawHdr* __restrict__ hdr, DrawOps ops) {
+    if (hdr->fail == 0) return;
+    for (int i = threadIdx.x; i < 2 * ops.n_at; i += blockDim.x) {
+        ops.at_calls[i] = make_int4(0, 0, 0, 0);
+        ops.at_sampled[i] = 0;
+    }
+    for (int i = threadIdx.x; i < 2 * ops.n_pt; i += blockDim.x) {
+        ops.pt_calls[i] = make_int4(0, 0, 0, 0);
+        if ((i & 1) == 0) {
+            ops.pt_scount[i >> 1] = 0;
+            ops.pt_spos[i >> 1] = 0;
+        }
     }
 }
 
@@ -1067,8 +1805,113 @@ struct AtWs {
     int* sampled;
     int4* calls;  // [2N] per choice() call: cnt (0: none), lowest recorded step, p_hi, offset
     int* jrec;    // [2N][kMaxKeep] recorded swaps
+    DrawCap cap;  // the chip-wide draws' capacity (cap.smax == 0: the walk only)
+    DrawBufs draw;
     size_t bytes;
 };
+
+// Capacity of the chip-wide draws for a stream of at most steps_cap Fisher-Yates
+// steps (each takes < 2 words on average): past it the plan fails and the walk runs.
+DrawCap draw_cap(int N, int64_t steps_cap) {
+    DrawCap c{};
+    if (N <= 0 || 2 * N > kDrawWalks || steps_cap <= 0) return c;
+    const double words = 2.0 * static_cast<double>(steps_cap) + 64.0 * std::sqrt(static_cast<double>(steps_cap)) + 4096.0;
+    // 1024-word segments, or 256-word ones when a stream fits 256 of them
+    const double s1024 = words / kSegLMax + 2.0, s256 = std::min(words / 256.0 + 2.0, 258.0);
+    c.smax = static_cast<int>(std::min(std::max(s1024, s256), static_cast<double>(kDrawSegMax - 1)));
+    c.nbmax = (kMtN + static_cast<int>(std::min(words + 4.0 * kSegLMax, 1.1e6))) / kMtN + 2;
+    c.tabmax = static_cast<int>(std::min<int64_t>(static_cast<int64_t>(c.smax) * kDrawDcap, int64_t{1} << 22));
+    c.premax = c.tabmax;
+    return c;
+}
+DrawBufs carve_draw(Carver& c, const DrawCap& cap) {
+    DrawBufs b{};
+    if (cap.smax == 0) return b;
+    b.hdr = c.take<DrawHdr>(1);
+    b.w_hi = c.take<int>(kDrawWalks);
+    b.w_cum = c.take<int>(kDrawWalks);
+    b.w_rec = c.take<int>(kDrawWalks);
+    b.w_row = c.take<int>(kDrawWalks);
+    b.s_lo = c.take<int>(cap.smax + 1);
+    b.s_d = c.take<int>(cap.smax + 1);
+    b.s_toff = c.take<int>(cap.smax + 1);
+    b.s_item = c.take<int>(cap.smax + 1);
+    b.g_poff = c.take<int>(cap.smax / kGrpG + 2);
+    b.kseg = c.take<int>(cap.smax + 1);
+    b.tab = c.take<uint16_t>(cap.tabmax);
+    b.pre = c.take<uint16_t>(cap.premax);
+    b.raw = c.take<uint32_t>(static_cast<size_t>(cap.nbmax) * kMtN);
+    b.tw = c.take<uint32_t>(static_cast<size_t>(cap.nbmax) * kMtN);
+    return b;
+}
+
+// The serial samplers' arguments (the walk: the fallback, and the path for
+// workspaces without a chip-wide part).
+struct SerialAt {
+    int N, A, n_sample, n_pos_max;
+    const int* pos_list;
+    const int* neg_list;
+    const int* npos;
+    const int* nneg;
+    int* sampled;
+    int4* calls;
+    int* jrec;
+};
+struct SerialPt {
+    int N, stride, n_sample, pos_per_image;
+    const int* pos_list;
+    const int* neg_list;
+    const int* npos;
+    const int* nneg;
+    int* scount;
+    int* spos;
+    int4* calls;
+    int* jrec;
+};
+
+// The draws of ops on the stream rng: chip-wide (setup, segment tables, group
+// composites, chain, exact walks of the recorded segments) with the serial
+// samplers behind, gated on the plan's fail flag; the serial samplers alone on
+// the "walk" path or without a chip-wide workspace part.
+int launch_draws(const DrawOps& ops, const SerialAt* at, const SerialPt* pt, uint32_t* rng, const DrawCap& cap,
+                 const DrawBufs& B, hipStream_t st) {
+    const int path = path_cfg().sampler;
+    const bool chip = path != kPathWalk && cap.smax > 0 && 2 * (ops.n_at + ops.n_pt) <= kDrawWalks;
+    if (chip) {
+        const float mult = path == kPathChipTight ? 0.0f : 5.0f;
+        const int slack = path == kPathChipTight ? 0 : 16;
+        hipLaunchKernelGGL(draw_setup_kernel, dim3(1), dim3(1024), 0, st, ops, rng, cap, mult, slack, B);
+        FRCNN_LAUNCH_CHECK("draw_setup_kernel");
+        hipLaunchKernelGGL(draw_table_kernel, dim3(2048), dim3(256), 0, st, B.hdr, B);  // 8 waves per SIMD
+        FRCNN_LAUNCH_CHECK("draw_table_kernel");
+        hipLaunchKernelGGL(draw_group_kernel, dim3((cap.smax + kGrpG - 1) / kGrpG), dim3(1024), 0, st, B.hdr, B);
+        FRCNN_LAUNCH_CHECK("draw_group_kernel");
+        hipLaunchKernelGGL(draw_chain_kernel, dim3(1), dim3(1024), 0, st, B.hdr, B);
+        FRCNN_LAUNCH_CHECK("draw_chain_kernel");
+        hipLaunchKernelGGL(draw_record_kernel, dim3(cap.smax), dim3(64), 0, st, B.hdr, B, ops, rng);
+        FRCNN_LAUNCH_CHECK("draw_record_kernel");
+        if (path == kPathChipOnly) {  // (tests) no walk behind: a failed plan leaves no calls
+            hipLaunchKernelGGL(draw_poison_kernel, dim3(1), dim3(256), 0, st, B.hdr, ops);
+            FRCNN_LAUNCH_CHECK("draw_poison_kernel");
+            return FRCNN_OK;
+        }
+    }
+    const int* gate = chip ? reinterpret_cast<const int*>(B.hdr) : nullptr;
+    if (at) {
+        hipLaunchKernelGGL(at_sample_kernel, dim3(1), dim3(kSampThreads), 0, st, at->N, at->A, at->n_sample,
+                           at->n_pos_max, at->pos_list, at->neg_list, at->npos, at->nneg, rng, at->sampled, at->calls,
+                           at->jrec, gate);
+        FRCNN_LAUNCH_CHECK("at_sample_kernel");
+    }
+    if (pt) {
+        hipLaunchKernelGGL(pt_sample_kernel, dim3(1), dim3(kSampThreads), 0, st, pt->N, pt->stride, pt->n_sample,
+                           pt->pos_per_image, pt->pos_list, pt->neg_list, pt->npos, pt->nneg, rng, pt->scount,
+                           pt->spos, pt->calls, pt->jrec, gate);
+        FRCNN_LAUNCH_CHECK("pt_sample_kernel");
+    }
+    return FRCNN_OK;
+}
+
 AtWs carve_at(void* ws, int N, int A, int Gp) {
     Carver c(ws);
     AtWs w{};
@@ -1089,8 +1932,22 @@ AtWs carve_at(void* ws, int N, int A, int Gp) {
     w.sampled = c.take<int>(2 * N);
     w.calls = c.take<int4>(2 * N);
     w.jrec = c.take<int>(static_cast<size_t>(2 * N) * kMaxKeep);
+    w.cap = draw_cap(N, static_cast<int64_t>(N) * A);
+    w.draw = carve_draw(c, w.cap);
     w.bytes = c.used();
     return w;
+}
+
+void at_ops(const AtWs& w, int N, int A, int n_sample, int n_pos_max, DrawOps& ops, SerialAt& at) {
+    ops.n_at = N;
+    ops.at_n_sample = n_sample;
+    ops.at_pos_max = n_pos_max;
+    ops.at_npos = w.npos;
+    ops.at_nneg = w.nneg;
+    ops.at_sampled = w.sampled;
+    ops.at_calls = w.calls;
+    ops.at_jrec = w.jrec;
+    at = SerialAt{N, A, n_sample, n_pos_max, w.pos_list, w.neg_list, w.npos, w.nneg, w.sampled, w.calls, w.jrec};
 }
 
 
@@ -1158,14 +2015,37 @@ extern "C" int frcnn_anchor_target_draw(int N, int A, int G, int n_sample, doubl
                   ws_bytes, w.bytes);
     hipStream_t st = as_stream(stream);
     if (rng_state) {
-        hipLaunchKernelGGL(at_sample_kernel, dim3(1), dim3(kSampThreads), 0, st, N, A, n_sample, n_pos_max,
-                           w.pos_list, w.neg_list, w.npos, w.nneg, rng_state, w.sampled, w.calls, w.jrec);
-        FRCNN_LAUNCH_CHECK("at_sample_kernel");
+        DrawOps ops{};
+        SerialAt at{};
+        at_ops(w, N, A, n_sample, n_pos_max, ops, at);
+        const int rc = launch_draws(ops, &at, nullptr, rng_state, w.cap, w.draw, st);
+        if (rc != FRCNN_OK) return rc;
     } else if (hipMemsetAsync(w.sampled, 0, sizeof(int) * 2 * N, st) != hipSuccess ||
                hipMemsetAsync(w.calls, 0, sizeof(int4) * 2 * N, st) != hipSuccess) {
         return check_launch("frcnn_anchor_target_draw memset");
     }
     return FRCNN_OK;
+}
+
+// The chip-wide draws' plan header of the last frcnn_anchor_target_draw on this
+// workspace (synchronous): out[9] = fail, walks, steps, segments, groups, state
+// blocks, start pos, widest domain, missed group; rc 1 when the workspace has no
+// chip-wide part (the walk only).
+static int draw_status(const DrawBufs& d, const DrawCap& cap, int* out) {
+    if (cap.smax == 0) return 1;
+    DrawHdr h{};
+    if (hipMemcpy(&h, d.hdr, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess) return check_launch("draw_status copy");
+    const int v[9] = {h.fail, h.nw, h.ktot, h.nseg, h.ngrp, h.nblk, h.off0, h.dmax, h.miss};
+    for (int i = 0; i < 9; ++i) out[i] = v[i];
+    return FRCNN_OK;
+}
+
+extern "C" int frcnn_anchor_target_draw_status(int N, int A, int G, const void* workspace, size_t ws_bytes,
+                                               int* out) {
+    FRCNN_REQUIRE(N > 0 && A > 0 && G >= 0 && out, "frcnn_anchor_target_draw_status: bad argument");
+    AtWs w = carve_at(const_cast<void*>(workspace), N, A, G > 0 ? G : 1);
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_anchor_target_draw_status: workspace too small");
+    return draw_status(w.draw, w.cap, out);
 }
 
 extern "C" int frcnn_anchor_target_finish(int N, int A, int G, const float* anchors, double* reg, int32_t* label,
@@ -1236,6 +2116,8 @@ struct PtWs {
     int* spos;
     int4* calls;
     int* jrec;
+    DrawCap cap;
+    DrawBufs draw;
     size_t bytes;
 };
 PtWs carve_pt(void* ws, int N, int Rp, int Gp, int n_sample) {
@@ -1255,8 +2137,25 @@ PtWs carve_pt(void* ws, int N, int Rp, int Gp, int n_sample) {
     w.spos = c.take<int>(N);
     w.calls = c.take<int4>(2 * N);
     w.jrec = c.take<int>(static_cast<size_t>(2 * N) * kMaxKeep);
+    w.cap = draw_cap(N, static_cast<int64_t>(N) * static_cast<int64_t>(stride));
+    w.draw = carve_draw(c, w.cap);
     w.bytes = c.used();
     return w;
+}
+
+void pt_ops(const PtWs& w, int N, int stride, int n_sample, int pos_per_image, int32_t* sample_count, DrawOps& ops,
+            SerialPt& pt) {
+    ops.n_pt = N;
+    ops.pt_n_sample = n_sample;
+    ops.pt_pos_per_image = pos_per_image;
+    ops.pt_npos = w.npos;
+    ops.pt_nneg = w.nneg;
+    ops.pt_calls = w.calls;
+    ops.pt_scount = sample_count;
+    ops.pt_spos = w.spos;
+    ops.pt_jrec = w.jrec;
+    pt = SerialPt{N, stride, n_sample, pos_per_image, w.pos_list, w.neg_list, w.npos, w.nneg, sample_count, w.spos,
+                  w.calls, w.jrec};
 }
 }  // namespace
 
@@ -1309,11 +2208,46 @@ extern "C" int frcnn_proposal_target_draw(int N, int Rp, int G, int n_sample, do
     hipStream_t st = as_stream(stream);
     const int stride = Rp + Gp;
     const int pos_per_image = static_cast<int>(std::nearbyint(n_sample * pos_ratio));  // np.round
-    hipLaunchKernelGGL(pt_sample_kernel, dim3(1), dim3(kSampThreads), 0, st, N, stride, n_sample,
-                       pos_per_image, w.pos_list, w.neg_list, w.npos, w.nneg, rng_state, sample_count, w.spos,
-                       w.calls, w.jrec);
-    FRCNN_LAUNCH_CHECK("pt_sample_kernel");
-    return FRCNN_OK;
+    DrawOps ops{};
+    SerialPt pt{};
+    pt_ops(w, N, stride, n_sample, pos_per_image, sample_count, ops, pt);
+    return launch_draws(ops, nullptr, &pt, rng_state, w.cap, w.draw, st);
+}
+
+extern "C" int frcnn_target_draws(int N, int A, int G_at, int n_sample_at, double pos_ratio_at, void* at_workspace,
+                                  size_t at_bytes, int Rp, int G_pt, int n_sample_pt, double pos_ratio_pt,
+                                  void* pt_workspace, size_t pt_bytes, int32_t* sample_count, uint32_t* rng_state,
+                                  void* stream) {
+    FRCNN_REQUIRE(N > 0 && N <= 65535 && A > 0 && G_at >= 0 && G_at <= kMaxG && Rp >= 0 && G_pt >= 0 &&
+                      G_pt <= kMaxG && n_sample_pt > 0 && n_sample_at > 0,
+                  "frcnn_target_draws: bad shape");
+    const int n_pos_max = static_cast<int>(pos_ratio_at * n_sample_at);
+    FRCNN_REQUIRE(n_sample_at - (n_pos_max < 0 ? 0 : n_pos_max) <= kMaxKeep && n_pos_max <= kMaxKeep,
+                  "frcnn_target_draws: n_sample_at must be in 1..%d per choice() call", kMaxKeep);
+    FRCNN_REQUIRE(Rp + G_pt <= kMaxKeep, "frcnn_target_draws: rois + gt must be <= %d", kMaxKeep);
+    FRCNN_REQUIRE(rng_state && sample_count, "frcnn_target_draws: null pointer");
+    AtWs aw = carve_at(at_workspace, N, A, G_at > 0 ? G_at : 1);
+    FRCNN_REQUIRE(at_workspace && at_bytes >= aw.bytes, "frcnn_target_draws: anchor workspace %zu < %zu", at_bytes,
+                  aw.bytes);
+    const int Gp = G_pt > 0 ? G_pt : 1;
+    PtWs pw = carve_pt(pt_workspace, N, Rp, Gp, n_sample_pt);
+    FRCNN_REQUIRE(pt_workspace && pt_bytes >= pw.bytes, "frcnn_target_draws: proposal workspace %zu < %zu", pt_bytes,
+                  pw.bytes);
+    const int pos_per_image = static_cast<int>(std::nearbyint(n_sample_pt * pos_ratio_pt));  // np.round
+    DrawOps ops{};
+    SerialAt at{};
+    SerialPt pt{};
+    at_ops(aw, N, A, n_sample_at, n_pos_max, ops, at);
+    pt_ops(pw, N, Rp + Gp, n_sample_pt, pos_per_image, sample_count, ops, pt);
+    return launch_draws(ops, &at, &pt, rng_state, aw.cap, aw.draw, as_stream(stream));
+}
+
+extern "C" int frcnn_proposal_target_draw_status(int N, int Rp, int G, int n_sample, const void* workspace,
+                                                 size_t ws_bytes, int* out) {
+    FRCNN_REQUIRE(N > 0 && Rp >= 0 && G >= 0 && n_sample > 0 && out, "frcnn_proposal_target_draw_status: bad argument");
+    PtWs w = carve_pt(const_cast<void*>(workspace), N, Rp, G > 0 ? G : 1, n_sample);
+    FRCNN_REQUIRE(workspace && ws_bytes >= w.bytes, "frcnn_proposal_target_draw_status: workspace too small");
+    return draw_status(w.draw, w.cap, out);
 }
 
 extern "C" int frcnn_proposal_target_finish(int N, int Rp, int G, int n_sample, const double* reg_mean,

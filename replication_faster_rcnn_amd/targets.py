@@ -137,6 +137,25 @@ def anchor_targets_draw(plan, n_sample=256, pos_ratio=0.5, rng=None):
         rng_state_from_device(rng, st)
 
 
+_STATUS_KEYS = ("fail", "walks", "steps", "segments", "groups", "blocks", "pos", "widest", "missed_group")
+
+
+def _draw_status(rc, buf):
+    if rc == 1:
+        return None  # no chip-wide part (> 128 images)
+    _lib.check(rc, "draw_status")
+    return dict(zip(_STATUS_KEYS, list(buf)))
+
+
+def anchor_targets_draw_status(plan):
+    """The chip-wide draws' plan of the last draw on ``plan`` (synchronous
+    diagnostic): fail 0 = the segment tables held; None = walk-only workspace."""
+    import ctypes
+    buf = (ctypes.c_int * 9)()
+    rc = _lib.load().frcnn_anchor_target_draw_status(plan.N, plan.A, plan.G, _lib.ptr(plan.ws), plan.ws.numel(), buf)
+    return _draw_status(rc, buf)
+
+
 def anchor_targets_finish(plan, out=None):
     """Final labels and regression targets after ``anchor_targets_draw``
     (utils/utils.py:146-150,203-204); ``out`` = caller-owned (reg, label)."""
@@ -272,6 +291,31 @@ def proposal_targets_draw(plan, pos_ratio=0.5, rng=None, count=None):
     if own:
         rng_state_from_device(rng, st)
     return count
+
+
+def target_draws(at_plan, pt_plan, rng, count=None, n_sample_at=256, pos_ratio_at=0.5, pos_ratio_pt=0.5):
+    """``anchor_targets_draw(at_plan)`` then ``proposal_targets_draw(pt_plan)`` on the
+    device stream ``rng`` as one pass (train.py:71 / :91: every AnchorTarget draw
+    before any ProposalTarget one; bit-identical to the two calls); both plans'
+    prepares must be ordered before it.  Returns the ProposalTarget count tensor."""
+    lib = _lib.load()
+    assert at_plan.N == pt_plan.N, "one batch of images"
+    if count is None:
+        count = torch.empty((pt_plan.N,), dtype=torch.int32, device=pt_plan.ws.device)
+    _lib.check(lib.frcnn_target_draws(at_plan.N, at_plan.A, at_plan.G, int(n_sample_at), float(pos_ratio_at),
+                                      _lib.ptr(at_plan.ws), at_plan.ws.numel(), pt_plan.Rp, pt_plan.G,
+                                      pt_plan.n_sample, float(pos_ratio_pt), _lib.ptr(pt_plan.ws), pt_plan.ws.numel(),
+                                      _lib.ptr(count), _lib.ptr(rng), _lib.stream_ptr()), "target_draws")
+    return count
+
+
+def proposal_targets_draw_status(plan):
+    """As ``anchor_targets_draw_status`` for the last proposal-target draw."""
+    import ctypes
+    buf = (ctypes.c_int * 9)()
+    rc = _lib.load().frcnn_proposal_target_draw_status(plan.N, plan.Rp, plan.G, plan.n_sample, _lib.ptr(plan.ws),
+                                                       plan.ws.numel(), buf)
+    return _draw_status(rc, buf)
 
 
 def proposal_targets_finish(plan, count, reg_normalize_mean=(0., 0., 0., 0.),

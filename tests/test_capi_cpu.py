@@ -67,7 +67,7 @@ def test_set_path_accepts_the_documented_paths_only():
           "roi_pool_bwd": ["auto", "ring", "plain"],
           "propose": ["auto", "hybrid", "lazy", "wide"],
           "roi_pool_fwd_store": ["auto", "temporal", "nt"],
-          "sampler": ["auto", "walk"],
+          "sampler": ["auto", "walk", "chip", "chip_only", "chip_tight"],
           "roi_pool_split": ["auto", "0", "7", "64"],
           "roi_pool_cg": ["auto", "4", "8", "16"]}
     try:
@@ -75,7 +75,7 @@ def test_set_path_accepts_the_documented_paths_only():
             for p in paths:
                 assert lib.frcnn_set_path(op.encode(), p.encode()) == 0, (op, p)
         for op, p in [("roi_pool_fwd_store", "streaming"), ("roi_pool_split", "65"), ("roi_pool_split", "x"),
-                      ("roi_pool_cg", "2"), ("sampler", "tiles"), ("sampler", "chip"), ("roi_pool_fwd", "key"),
+                      ("roi_pool_cg", "2"), ("sampler", "tiles"), ("sampler", "chip_wide"), ("roi_pool_fwd", "key"),
                       ("roi_pool_fwd", "pair"), ("roi_pool_bwd", "band"), ("no_such_op", "auto")]:
             assert lib.frcnn_set_path(op.encode(), p.encode()) == -1, (op, p)
             assert p.encode() in lib.frcnn_last_error()
