@@ -1882,7 +1882,10 @@ int launch_draws(const DrawOps& ops, const SerialAt* at, const SerialPt* pt, uin
         const int slack = path == kPathChipTight ? 0 : 16;
         hipLaunchKernelGGL(draw_setup_kernel, dim3(1), dim3(1024), 0, st, ops, rng, cap, mult, slack, B);
         FRCNN_LAUNCH_CHECK("draw_setup_kernel");
-        hipLaunchKernelGGL(draw_table_kernel, dim3(2048), dim3(256), 0, st, B.hdr, B);  // 8 waves per SIMD
+#ifndef FRCNN_TABLE_WGS
+#define FRCNN_TABLE_WGS 2048  // 8 waves per SIMD
+#endif
+        hipLaunchKernelGGL(draw_table_kernel, dim3(FRCNN_TABLE_WGS), dim3(256), 0, st, B.hdr, B);
         FRCNN_LAUNCH_CHECK("draw_table_kernel");
         hipLaunchKernelGGL(draw_group_kernel, dim3((cap.smax + kGrpG - 1) / kGrpG), dim3(1024), 0, st, B.hdr, B);
         FRCNN_LAUNCH_CHECK("draw_group_kernel");
