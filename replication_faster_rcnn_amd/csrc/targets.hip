@@ -718,18 +718,9 @@ __device__ void fy_final(int cnt, int rec_lo, int p_lo, int p_hi, const int* J, 
 // utils/utils.py:190-202.  Kept anchors are marked in keep[n][a] (zeroed by
 // the caller); pos_sampled / neg_sampled record whether a call happened.
 
-__global__ __launch_bounds__(kSampThreads) void at_sample_kernel(
-    int N, int A, int n_sample, int n_pos_max, const int* __restrict__ pos_list,
-    const int* __restrict__ neg_list, const int* __restrict__ npos, const int* __restrict__ nneg,
-    uint32_t* __restrict__ rng, int* __restrict__ sampled, int4* __restrict__ calls, int* __restrict__ jrec,
-    const int* __restrict__ gate) {
-    __shared__ WalkLds S;
-    __shared__ int J[kMaxKeep];
-    if (gate && *gate == 0) return;  // the chip-wide draws succeeded (draw_chain_kernel)
-    SPROF_T0();
-    Stream st;
-    stream_load(S, st, rng);
-    __syncthreads();
+__device__ void at_draws(WalkLds& S, Stream& st, int* J, int N, int n_sample, int n_pos_max,
+                         const int* __restrict__ npos, const int* __restrict__ nneg, int* __restrict__ sampled,
+                         int4* __restrict__ calls, int* __restrict__ jrec) {
     for (int n = 0; n < N; ++n) {
         const int P = npos[n];
         const int Q = nneg[n];
@@ -754,6 +745,21 @@ __global__ __launch_bounds__(kSampThreads) void at_sample_kernel(
             __syncthreads();
         }
     }
+}
+
+__global__ __launch_bounds__(kSampThreads) void at_sample_kernel(
+    int N, int A, int n_sample, int n_pos_max, const int* __restrict__ pos_list,
+    const int* __restrict__ neg_list, const int* __restrict__ npos, const int* __restrict__ nneg,
+    uint32_t* __restrict__ rng, int* __restrict__ sampled, int4* __restrict__ calls, int* __restrict__ jrec,
+    const int* __restrict__ gate) {
+    __shared__ WalkLds S;
+    __shared__ int J[kMaxKeep];
+    if (gate && *gate == 0) return;  // the chip-wide draws succeeded (draw_chain_kernel)
+    SPROF_T0();
+    Stream st;
+    stream_load(S, st, rng);
+    __syncthreads();
+    at_draws(S, st, J, N, n_sample, n_pos_max, npos, nneg, sampled, calls, jrec);
     stream_store(S, st, rng);
     SPROF_DT(6);
 }
@@ -878,17 +884,9 @@ __global__ __launch_bounds__(1024) void pt_iou_kernel(
 
 // One workgroup: the two choice() calls of utils/utils.py:248-258 per image,
 // in image order; sample order = pos perm prefix, then neg perm prefix.
-__global__ __launch_bounds__(kSampThreads) void pt_sample_kernel(
-    int N, int stride, int n_sample, int pos_per_image, const int* __restrict__ pos_list,
-    const int* __restrict__ neg_list, const int* __restrict__ npos, const int* __restrict__ nneg,
-    uint32_t* __restrict__ rng, int* __restrict__ scount,
-    int* __restrict__ spos, int4* __restrict__ calls, int* __restrict__ jrec, const int* __restrict__ gate) {
-    __shared__ WalkLds S;
-    __shared__ int J[kMaxKeep];
-    if (gate && *gate == 0) return;  // the chip-wide draws succeeded (draw_chain_kernel)
-    Stream st;
-    stream_load(S, st, rng);
-    __syncthreads();
+__device__ void pt_draws(WalkLds& S, Stream& st, int* J, int N, int n_sample, int pos_per_image,
+                         const int* __restrict__ npos, const int* __restrict__ nneg, int* __restrict__ scount,
+                         int* __restrict__ spos, int4* __restrict__ calls, int* __restrict__ jrec) {
     for (int n = 0; n < N; ++n) {
         const int P = npos[n], Q = nneg[n];
         const int kp = P < pos_per_image ? P : pos_per_image;
@@ -911,6 +909,39 @@ __global__ __launch_bounds__(kSampThreads) void pt_sample_kernel(
             spos[n] = kp;
         }
     }
+}
+
+__global__ __launch_bounds__(kSampThreads) void pt_sample_kernel(
+    int N, int stride, int n_sample, int pos_per_image, const int* __restrict__ pos_list,
+    const int* __restrict__ neg_list, const int* __restrict__ npos, const int* __restrict__ nneg,
+    uint32_t* __restrict__ rng, int* __restrict__ scount,
+    int* __restrict__ spos, int4* __restrict__ calls, int* __restrict__ jrec, const int* __restrict__ gate) {
+    __shared__ WalkLds S;
+    __shared__ int J[kMaxKeep];
+    if (gate && *gate == 0) return;  // the chip-wide draws succeeded (draw_chain_kernel)
+    Stream st;
+    stream_load(S, st, rng);
+    __syncthreads();
+    pt_draws(S, st, J, N, n_sample, pos_per_image, npos, nneg, scount, spos, calls, jrec);
+    stream_store(S, st, rng);
+}
+
+// Both creators' serial draws in one launch (the walk behind frcnn_target_draws'
+// chip-wide pass: one gate check, one workgroup waiting for its LDS, not two).
+__global__ __launch_bounds__(kSampThreads) void target_sample_kernel(
+    int n_at, int at_n_sample, int at_pos_max, const int* __restrict__ at_npos, const int* __restrict__ at_nneg,
+    int* __restrict__ at_sampled, int4* __restrict__ at_calls, int* __restrict__ at_jrec, int n_pt,
+    int pt_n_sample, int pt_pos_per_image, const int* __restrict__ pt_npos, const int* __restrict__ pt_nneg,
+    int* __restrict__ pt_scount, int* __restrict__ pt_spos, int4* __restrict__ pt_calls,
+    int* __restrict__ pt_jrec, uint32_t* __restrict__ rng, const int* __restrict__ gate) {
+    __shared__ WalkLds S;
+    __shared__ int J[kMaxKeep];
+    if (gate && *gate == 0) return;
+    Stream st;
+    stream_load(S, st, rng);
+    __syncthreads();
+    at_draws(S, st, J, n_at, at_n_sample, at_pos_max, at_npos, at_nneg, at_sampled, at_calls, at_jrec);
+    pt_draws(S, st, J, n_pt, pt_n_sample, pt_pos_per_image, pt_npos, pt_nneg, pt_scount, pt_spos, pt_calls, pt_jrec);
     stream_store(S, st, rng);
 }
 
@@ -1611,6 +1642,7 @@ __global__ __launch_bounds__(64) void draw_record_kernel(const DrawHdr* __restri
         return l;
     };
     const int L = hdr->seg_l;
+    int cw = walk_of(K0);  // the walk of the chunk's first K, carried across chunks
     const uint32_t* wp = B.tw + static_cast<size_t>(s) * L;
     uint32_t wv[kSegLMax / 64];  // every chunk's word loaded at once (one memory latency)
 #pragma unroll
@@ -1620,7 +1652,8 @@ __global__ __launch_bounds__(64) void draw_record_kernel(const DrawHdr* __restri
     for (int ch = 0; ch < kSegLMax / 64; ++ch) {
         if (ch * 64 >= L || Kc >= K1) break;
         const uint32_t w = wv[ch];
-        const int c0 = walk_of(Kc);
+        while (cw < nw && cum[cw] <= Kc) ++cw;
+        const int c0 = cw;
         const bool one = c0 < nw && Kc + 64 <= cum[c0];  // the chunk stays in walk c0
         const uint32_t b0 = c0 < nw ? static_cast<uint32_t>(cum[c0] - Kc) : 0u;
         const float pa = (static_cast<float>(b0) + 1.0f) / (static_cast<float>(mask_for(b0 | 1u)) + 1.0f);
@@ -1900,6 +1933,14 @@ int launch_draws(const DrawOps& ops, const SerialAt* at, const SerialPt* pt, uin
         }
     }
     const int* gate = chip ? reinterpret_cast<const int*>(B.hdr) : nullptr;
+    if (at && pt) {
+        hipLaunchKernelGGL(target_sample_kernel, dim3(1), dim3(kSampThreads), 0, st, at->N, at->n_sample,
+                           at->n_pos_max, at->npos, at->nneg, at->sampled, at->calls, at->jrec, pt->N, pt->n_sample,
+                           pt->pos_per_image, pt->npos, pt->nneg, pt->scount, pt->spos, pt->calls, pt->jrec, rng,
+                           gate);
+        FRCNN_LAUNCH_CHECK("target_sample_kernel");
+        return FRCNN_OK;
+    }
     if (at) {
         hipLaunchKernelGGL(at_sample_kernel, dim3(1), dim3(kSampThreads), 0, st, at->N, at->A, at->n_sample,
                            at->n_pos_max, at->pos_list, at->neg_list, at->npos, at->nneg, rng, at->sampled, at->calls,
