@@ -73,6 +73,8 @@ def parse():
     ap.add_argument("--streams", type=int, default=2, choices=(1, 2),
                     help="2: the proposal layer of step k+1 runs on its own HIP stream beside "
                          "step k's RoIPool (each step still does all of its work)")
+    ap.add_argument("--target-bufs", type=int, default=3,
+                    help="cfg5: target-creator workspaces in rotation (step k's prepares reuse step k-N's)")
     ap.add_argument("--rng-waits", choices=["front", "split"], default="front",
                     help="cfg5: the draws' stream waits for both prepares before its first sampler "
                          "(front) or for each before its sampler (split)")
@@ -665,27 +667,28 @@ def train_step_fn(args, c, sets, base, first_image, ev):
     state = {}
     # AnchorTargetCreator's RNG-free half (IoU, labels, candidate lists) of step
     # k runs on the proposal stream, ahead of step k's proposals and beside step
-    # k-1's draws; two workspaces alternate
+    # k-1's draws; --target-bufs workspaces rotate
     A_ = anchors.size(0)
-    at_ws = [targets.anchor_targets_workspace(N, A_, boxes.size(1), dev) for _ in range(2)]
+    nb = getattr(args, "target_bufs", 3)  # step k's prepares wait for step k - nb's draws and finishes
+    at_ws = [targets.anchor_targets_workspace(N, A_, boxes.size(1), dev) for _ in range(nb)]
     at_out = [(torch.empty((N, A_, 4), dtype=torch.float64, device=dev),
-               torch.empty((N, A_), dtype=torch.int32, device=dev)) for _ in range(2)]
-    prep_ready = [torch.cuda.Event() for _ in range(2)]
-    sample_done = [None, None]
-    sample_ev = [torch.cuda.Event() for _ in range(2)]
+               torch.empty((N, A_), dtype=torch.int32, device=dev)) for _ in range(nb)]
+    prep_ready = [torch.cuda.Event() for _ in range(nb)]
+    sample_done = [None] * nb
+    sample_ev = [torch.cuda.Event() for _ in range(nb)]
     # ProposalTargetCreator's RNG-free half (IoU, fg / bg lists) follows the
     # proposals on their stream; the draws' stream only runs the draws
-    pt_ws = [targets.proposal_targets_workspace(N, c["post_nms"], boxes.size(1), S, dev) for _ in range(2)]
+    pt_ws = [targets.proposal_targets_workspace(N, c["post_nms"], boxes.size(1), S, dev) for _ in range(nb)]
     pt_out = [(torch.empty((N, S, 4), dtype=torch.float64, device=dev),
                torch.empty((N, S, 4), dtype=torch.float64, device=dev),
                torch.empty((N, S), dtype=torch.float64, device=dev),
-               torch.empty((N,), dtype=torch.int32, device=dev)) for _ in range(2)]
-    pt_done = [None, None]
-    pt_ev = [torch.cuda.Event() for _ in range(2)]
+               torch.empty((N,), dtype=torch.int32, device=dev)) for _ in range(nb)]
+    pt_done = [None] * nb
+    pt_ev = [torch.cuda.Event() for _ in range(nb)]
     k_step = [0]
 
     def step(timed):
-        j = k_step[0] % 2
+        j = k_step[0] % nb
         sc, de, x = sets[k_step[0] % len(sets)]
         k_step[0] += 1
         with torch.cuda.stream(s_prep):
@@ -727,11 +730,11 @@ def train_step_fn(args, c, sets, base, first_image, ev):
             s_pool.wait_event(pt_drawn)
             reg_t, lab = targets.anchor_targets_finish(plan, out=at_out[j])
             sample_ev[j].record(s_pool)
-            sample_done[j] = sample_ev[j]   # at_ws[j] free for step k+2's prepare
+            sample_done[j] = sample_ev[j]   # at_ws[j] free for step k+nb's prepare
             s_roi, s_reg, s_lab = targets.proposal_targets_finish(pplan, s_cnt, out=pt_out[j][:3])
             sample_rois = s_roi.float().view(-1, 4)          # train.py:86,102,107
             pt_ev[j].record(s_pool)
-            pt_done[j] = pt_ev[j]           # pt_ws[j], pt_out[j] free for step k+2
+            pt_done[j] = pt_ev[j]           # pt_ws[j], pt_out[j] free for step k+nb
             if timed:
                 e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
                 e[0].record(s_pool)
@@ -940,7 +943,7 @@ def main():
                    "parallelism": f"dp{world} (per-image sharding)", "streams": args.streams,
                    "prop_streams": args.prop_streams if (args.streams == 2 and not train) else 1,
                    "pool_on": args.pool_on if (args.streams == 2 and not train) else None,
-                   "host_io": bool(args.host_io), "rng_waits": args.rng_waits, "roi_path": args.roi_path, "roi_cg": args.roi_cg, "roi_split": args.roi_split, "roi_store": args.roi_store,
+                   "host_io": bool(args.host_io), "rng_waits": args.rng_waits, "target_bufs": getattr(args, "target_bufs", 3) if train else None, "roi_path": args.roi_path, "roi_cg": args.roi_cg, "roi_split": args.roi_split, "roi_store": args.roi_store,
                    "prop_cus": args.prop_cus if (args.streams == 2 and not train) else 0,
                    "propose_path": args.propose_path,
                    "collective": (None if world == 1 else

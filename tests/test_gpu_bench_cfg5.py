@@ -24,10 +24,10 @@ pytestmark = pytest.mark.gpu
 def test_benched_cfg5_steps_vs_oracle(rng_guard):
     dev = torch.device("cuda", 0)
     cfg = "cfg5"
-    N, S, steps = 16, 128, 3
+    N, S, steps = 16, 128, 4  # (4 steps: the 3 rotating target workspaces wrap once)
     c, sets, _ = bench.make_input_sets(cfg, range(N), dev, 2)
     base = A.generate_anchor_base_device(anchor_scales=c["scales"])
-    args = types.SimpleNamespace(streams=2, rng_waits="front")
+    args = types.SimpleNamespace(streams=2, rng_waits="front", target_bufs=3)
     ev = {"fwd": [], "bwd": [], "draw": [], "i": 0, "pairs": []}
     step = bench.train_step_fn(args, c, sets, base, 0, ev)   # seeds numpy's global RNG with 0
     st0 = np.random.get_state()
