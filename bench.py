@@ -73,6 +73,8 @@ def parse():
     ap.add_argument("--streams", type=int, default=2, choices=(1, 2),
                     help="2: the proposal layer of step k+1 runs on its own HIP stream beside "
                          "step k's RoIPool (each step still does all of its work)")
+    ap.add_argument("--prep-stream", choices=["prop", "own"], default="prop",
+                    help="cfg5: AnchorTarget's prepare on the proposals' stream or a fourth stream")
     ap.add_argument("--target-bufs", type=int, default=3,
                     help="cfg5: target-creator workspaces in rotation (step k's prepares reuse step k-N's)")
     ap.add_argument("--rng-waits", choices=["front", "split"], default="front",
@@ -663,7 +665,9 @@ def train_step_fn(args, c, sets, base, first_image, ev):
         s_prop = s_rng = s_pool = torch.cuda.current_stream()
     else:  # three streams: HIP maps streams onto 4 hardware queues (one is torch's default)
         s_prop, s_rng, s_pool = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
-    s_prep = s_prop
+    # AnchorTargetCreator's prepare on the proposals' stream (default) or its own: HIP maps
+    # streams onto 4 hardware queues, so a fourth stream shares one with another stream
+    s_prep = torch.cuda.Stream() if (args.streams != 1 and getattr(args, "prep_stream", "prop") == "own") else s_prop
     state = {}
     # AnchorTargetCreator's RNG-free half (IoU, labels, candidate lists) of step
     # k runs on the proposal stream, ahead of step k's proposals and beside step
