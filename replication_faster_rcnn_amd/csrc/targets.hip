@@ -1911,7 +1911,10 @@ int launch_draws(const DrawOps& ops, const SerialAt* at, const SerialPt* pt, uin
     const int path = path_cfg().sampler;
     const bool chip = path != kPathWalk && cap.smax > 0 && 2 * (ops.n_at + ops.n_pt) <= kDrawWalks;
     if (chip) {
-        const float mult = path == kPathChipTight ? 0.0f : 5.0f;
+#ifndef FRCNN_DRAW_SIGMAS
+#define FRCNN_DRAW_SIGMAS 4.0f  // domain half-width in sigma_W (worst of 140 simulated cfg5 paths: 3.7)
+#endif
+        const float mult = path == kPathChipTight ? 0.0f : FRCNN_DRAW_SIGMAS;
         const int slack = path == kPathChipTight ? 0 : 16;
         hipLaunchKernelGGL(draw_setup_kernel, dim3(1), dim3(1024), 0, st, ops, rng, cap, mult, slack, B);
         FRCNN_LAUNCH_CHECK("draw_setup_kernel");
