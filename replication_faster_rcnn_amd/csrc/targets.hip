@@ -183,12 +183,25 @@ __global__ __launch_bounds__(1024) void at_label_kernel(
     const int G = gcount[n];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     for (int g = tid; g < G; g += 1024) {
+        // the block partials in order, eight loads in flight at a time (one round
+        // trip per eight blocks, not per block); the fold order is unchanged
         ArgMax c{0.0, 0, 0};
-        for (int b = 0; b < nblk; ++b) {
-            const size_t o = (static_cast<size_t>(n) * nblk + b) * Gp + g;
-            const double v = col_v[o];
-            ArgMax x{v, col_i[o], v != v};
-            c = b == 0 ? x : am_combine(c, x);
+        for (int b0 = 0; b0 < nblk; b0 += 8) {
+            double vv[8];
+            int ii[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const size_t o = (static_cast<size_t>(n) * nblk + min(b0 + u, nblk - 1)) * Gp + g;
+                vv[u] = col_v[o];
+                ii[u] = col_i[o];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (b0 + u < nblk) {
+                    const ArgMax x{vv[u], ii[u], vv[u] != vv[u]};
+                    c = b0 + u == 0 ? x : am_combine(c, x);
+                }
+            }
         }
         s_garg[g] = c.i;
     }
