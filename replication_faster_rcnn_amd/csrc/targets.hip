@@ -145,14 +145,24 @@ __global__ __launch_bounds__(256) void at_iou_kernel(const float* __restrict__ a
             best.i = g;
             best.nan = v != v;
         }
-        // column partial: first anchor of this block with the best value
-        ArgMax c{va ? v : -INFINITY, va ? a : 0x7fffffff, (va && v != v) ? 1 : 0};
-        for (int o = 1; o < 64; o <<= 1) {  // ordered reduction over lanes
-            ArgMax other;
-            other.v = __shfl_down(c.v, o, 64);
-            other.i = __shfl_down(c.i, o, 64);
-            other.nan = __shfl_down(c.nan, o, 64);
-            if ((lane & (2 * o - 1)) == 0 && lane + o < 64) c = am_combine(c, other);
+        // column partial: the wave's first anchor with the best value, as the ordered
+        // am_combine fold gives it -- the first NaN if any, else the first lane at the
+        // maximum (ties and -0.0 / 0.0 keep the earlier lane; the invalid lanes, a
+        // suffix, hold -inf and index 0x7fffffff) -- from two ballots and a max
+        const double cvv = va ? v : -INFINITY;
+        const uint64_t nanb = __builtin_amdgcn_ballot_w64(va && v != v);
+        ArgMax c;
+        if (nanb) {
+            const int f = __ffsll(static_cast<unsigned long long>(nanb)) - 1;
+            c = ArgMax{__builtin_nan(""), static_cast<int>(blockIdx.x) * 256 + wid * 64 + f, 1};
+        } else {
+            double m = cvv;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) m = fmax(m, __shfl_xor(m, o, 64));
+            const uint64_t eq = __builtin_amdgcn_ballot_w64(cvv == m);
+            const int f = __ffsll(static_cast<unsigned long long>(eq)) - 1;
+            const int af = static_cast<int>(blockIdx.x) * 256 + wid * 64 + f;
+            c = ArgMax{m, af < A ? af : 0x7fffffff, 0};
         }
         if (lane == 0) wred[wid][g] = c;
     }
