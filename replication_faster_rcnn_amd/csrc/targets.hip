@@ -188,7 +188,6 @@ __global__ __launch_bounds__(1024) void at_label_kernel(
     int32_t* __restrict__ row_arg, int8_t* __restrict__ label0, int* __restrict__ pos_list,
     int* __restrict__ neg_list, int* __restrict__ npos, int* __restrict__ nneg) {
     __shared__ int s_garg[kMaxG];
-    __shared__ int s_w[16];
     const int n = blockIdx.x;
     const int G = gcount[n];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -234,34 +233,46 @@ __global__ __launch_bounds__(1024) void at_label_kernel(
         }
     }
     __syncthreads();
-    // ordered compaction of label==1 and label==0 positions
-    int pbase = 0, nbase = 0;
-    for (int a0 = 0; a0 < A; a0 += 1024) {
-        const int a = a0 + tid;
-        const int8_t l = a < A ? lab[a] : -1;
-        const uint64_t bp = __ballot(l == 1), bn = __ballot(l == 0);
-        const int cp = __popcll(bp), cn = __popcll(bn);
-        if (lane == 0) s_w[wid] = cp | (cn << 16);
-        __syncthreads();
-        int bpp = 0, bnn = 0, tp = 0, tn = 0;
-        for (int w = 0; w < 16; ++w) {
-            const int v = s_w[w];
-            if (w < wid) {
-                bpp += v & 0xffff;
-                bnn += v >> 16;
-            }
-            tp += v & 0xffff;
-            tn += v >> 16;
-        }
-        if (l == 1) pos_list[static_cast<size_t>(n) * A + pbase + bpp + __popcll(bp & lanemask_lt())] = a;
-        if (l == 0) neg_list[static_cast<size_t>(n) * A + nbase + bnn + __popcll(bn & lanemask_lt())] = a;
-        pbase += tp;
-        nbase += tn;
-        __syncthreads();
+    // ordered compaction of label==1 and label==0 positions: thread t counts its run
+    // of anchors [t * per, (t + 1) * per), one block-wide exclusive scan of the
+    // counts, then each thread writes its run in order (one barrier round, not one
+    // per 1024 anchors)
+    const int per = (A + 1023) / 1024;
+    const int r0 = min(A, tid * per), r1 = min(A, r0 + per);
+    int cp = 0, cn = 0;
+    for (int a = r0; a < r1; ++a) {
+        const int8_t l = lab[a];
+        cp += l == 1;
+        cn += l == 0;
+    }
+    long long both = static_cast<long long>(cp) | (static_cast<long long>(cn) << 32);  // (no carries: < 2^31 each)
+    long long inc = both;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const long long u = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += u;
+    }
+    __shared__ long long s_wt[16];
+    if (lane == 63) s_wt[wid] = inc;
+    __syncthreads();
+    long long pre = 0, tot = 0;
+    for (int w = 0; w < 16; ++w) {
+        const long long x = s_wt[w];
+        if (w < wid) pre += x;
+        tot += x;
+    }
+    const long long ex = pre + inc - both;
+    int pp = static_cast<int>(ex & 0xffffffffll), pn = static_cast<int>(ex >> 32);
+    int* pl = pos_list + static_cast<size_t>(n) * A;
+    int* nl = neg_list + static_cast<size_t>(n) * A;
+    for (int a = r0; a < r1; ++a) {
+        const int8_t l = lab[a];
+        if (l == 1) pl[pp++] = a;
+        if (l == 0) nl[pn++] = a;
     }
     if (tid == 0) {
-        npos[n] = pbase;
-        nneg[n] = nbase;
+        npos[n] = static_cast<int>(tot & 0xffffffffll);
+        nneg[n] = static_cast<int>(tot >> 32);
     }
 }
 
